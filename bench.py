@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Benchmark of the E-RAFT CorrBlock hot path on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch: CorrBlock build (fp32-MFMA GEMM + fused
+pyramid) followed by the 12 GRU-iteration lookups, exactly the call pattern of ERAFT.forward
+(eraft.py:107, 126-128), with inputs already resident in HBM.  Workload at N=1 = BASELINE
+configs[1]: DSEC 480x640 (fmaps 256 x 60 x 80), batch 16, warm-start coordinates (12 distinct
+coordinate fields = coords_grid + smooth flow + per-iteration jitter).  N>1 (configs[3]): one
+process per GPU, each with its own batch of pairs, no data-path collective ("weak" scaling).
+
+    python bench.py [--gpus N --steps K --warmup W --batch 16 --no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+
+Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP-event timed over the timed
+region) and `cpu_baseline` (the torch-CPU restatement of the reference, oracle/torch_ref.py, timed
+on this host's cores on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "flow pairs/sec (DSEC 480×640, 12 iters) at 1/8 GPUs; CorrBlock % roofline"
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix, spec (dense)
+PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak, spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=16, help="frame pairs per GPU")
+    ap.add_argument("--height", type=int, default=60, help="fmap rows (480/8)")
+    ap.add_argument("--width", type=int, default=80, help="fmap cols (640/8)")
+    ap.add_argument("--dim", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=12)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    return ap.parse_args()
+
+
+def algorithmic(B, D, H, W, L=4, r=4):
+    """build flops 2*B*Q^2*D; lookup bytes B*Q*[L(2r+2)^2*4 + L(2r+1)^2*4 + 8]."""
+    Q = H * W
+    flops = 2.0 * B * Q * Q * D
+    look_bytes = B * Q * (L * (2 * r + 2) ** 2 * 4 + L * (2 * r + 1) ** 2 * 4 + 2 * 4)
+    return flops, look_bytes
+
+
+def make_inputs(B, D, H, W, iters, device, seed):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    f1 = torch.randn((B, D, H, W), generator=g, device=device)
+    f2 = torch.randn((B, D, H, W), generator=g, device=device)
+    import eraft_amd
+    base = eraft_amd.coords_grid(B, H, W, device=device)
+    # warm start: smooth initial flow (sigma ~3 px at 1/8 res) plus per-iteration refinement
+    init = torch.nn.functional.avg_pool2d(torch.randn((B, 2, H, W), generator=g, device=device) * 9.0,
+                                          5, stride=1, padding=2)
+    coords = [(base + init + 0.5 * torch.randn((B, 2, H, W), generator=g, device=device)).contiguous()
+              for _ in range(iters)]
+    return f1, f2, coords
+
+
+def cpu_baseline(B, D, H, W, iters, seconds):
+    """torch-CPU restatement of the reference (oracle/torch_ref.py), bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from torch_ref import TorchCpuCorrBlock
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    torch.set_num_threads(cores)
+    nb = min(B, 4)
+    g = torch.Generator().manual_seed(7)
+    f1 = torch.randn((nb, D, H, W), generator=g)
+    f2 = torch.randn((nb, D, H, W), generator=g)
+    ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+    base = torch.stack([xs, ys]).float()[None].repeat(nb, 1, 1, 1)
+    coords = [base + 3.0 * torch.randn((nb, 2, H, W), generator=g) for _ in range(iters)]
+
+    def step():
+        blk = TorchCpuCorrBlock(f1, f2)
+        for c in coords:
+            blk(c)
+
+    step()  # warm-up
+    pairs, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        pairs += nb
+        el = time.perf_counter() - t0
+        if el >= seconds or pairs >= 64:
+            break
+    return {"value": pairs / el, "unit": "pairs/s", "cores": cores, "kind": "port",
+            "sample": f"{pairs} DSEC pairs ({nb} per step, fmap {D}x{H}x{W}, build + {iters} lookups) "
+                      f"in {el:.1f} s; torch {torch.__version__} CPU ops = reference's ATen ops"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    import eraft_amd
+
+    B, D, H, W, iters = a.batch, a.dim, a.height, a.width, a.iters
+    f1, f2, coords = make_inputs(B, D, H, W, iters, device, seed=1234 + rank)
+    stream = torch.cuda.current_stream(device)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        blk = eraft_amd.CorrBlock(f1, f2, num_levels=4, radius=4)
+        if ev is not None:
+            ev[1].record(stream)
+        for c in coords:
+            blk(c)
+        if ev is not None:
+            ev[2].record(stream)
+        return blk
+
+    with torch.no_grad():
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+        t0 = time.perf_counter()
+        for k in range(a.steps):
+            step(evs[k])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+
+    build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps
+    look_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps / iters
+    if world > 1:
+        t = torch.tensor([elapsed, build_ms, look_ms], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, build_ms, look_ms = t.tolist()
+
+    flops, look_bytes = algorithmic(B, D, H, W)
+    build_tf = flops / (build_ms * 1e-3) / 1e12
+    look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
+    kernels = {
+        "build": {"bound": "mfma", "achieved": round(build_tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
+                  "unit": "TFLOP/s", "frac": round(build_tf / PEAK_FP32_MFMA_TFLOPS, 4),
+                  "ms_per_launch": round(build_ms, 4), "work_per_launch": f"{flops:.4g} flop"},
+        "lookup": {"bound": "hbm", "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                   "frac": round(look_gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(look_ms, 4),
+                   "launches_per_step": iters, "work_per_launch": f"{look_bytes:.4g} B"},
+    }
+    dom = "build" if build_ms >= look_ms * iters else "lookup"
+    roof = {k: kernels[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")}
+    roof["kernel"] = dom
+    roof["traffic"] = None
+    ideal_s = flops / (PEAK_FP32_MFMA_TFLOPS * 1e12) + iters * look_bytes / (PEAK_HBM_GBS * 1e9)
+    pairs = world * B * a.steps
+    res = {
+        "metric": METRIC, "value": round(pairs / elapsed, 2), "unit": "pairs/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (randn fmaps, coords_grid + smooth warm-start flow)",
+        "config": {"workload": f"DSEC 480x640 CorrBlock build + {iters} lookups, warm-start, "
+                               f"batch {B} per GPU (BASELINE configs[1]; N>1 = configs[3])",
+                   "global_batch": world * B, "fmap": [D, H, W], "levels": 4, "radius": 4,
+                   "parallelism": f"dp{world} batch-sharded, no collective"},
+        "roofline": roof,
+        "kernels": kernels,
+        "corrblock_frac": round(ideal_s / (elapsed / a.steps), 4),
+    }
+    if rank == 0 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(B, D, H, W, iters, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,87 @@
+"""ctypes binding of libecorr.so (C ABI: include/ecorr.h).
+
+torch is imported first on purpose: torch ships its own libamdhip64.so (SONAME libamdhip64.so.7);
+loading libecorr.so afterwards makes the dynamic linker reuse that already-loaded runtime, so the
+kernels run in torch's HIP context on torch's streams and caching-allocator pointers.
+
+There is no fallback: if libecorr.so is missing or was built for another target, every entry point
+raises.  Build it with `make -C e-raft_amd/csrc` or `python -c "import __graft_entry__ as g; g.build()"`.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see above)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
+ABI_VERSION = 1
+MAX_LEVELS = 16
+
+ECORR_OK = 0
+ECORR_EINVAL = -1
+ECORR_ESHAPE = -2
+ECORR_ERADIUS = -3
+ECORR_ELEVELS = -4
+
+_lib = None
+
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_p = ctypes.c_void_p
+
+SYMBOLS = {
+    # name: (restype, argtypes)
+    "ecorr_abi_version": (_i, []),
+    "ecorr_strerror": (ctypes.c_char_p, [_i]),
+    "ecorr_pyramid_layout": (_i, [_i64, _i, _i, _i, ctypes.POINTER(_i), ctypes.POINTER(_i),
+                                  ctypes.POINTER(_i64)]),
+    "ecorr_build": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
+    "ecorr_lookup": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
+    "ecorr_bilinear_sampler": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _p]),
+    "ecorr_coords_grid": (_i, [_i, _i, _i, _p, _p]),
+}
+
+
+def lib():
+    """The loaded libecorr.so (raises if it is absent: no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"eraft_amd: {LIB_PATH} is not built; run `make -C e-raft_amd/csrc` "
+                "(hipcc --offload-arch=gfx950).  There is no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SYMBOLS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = L.ecorr_abi_version()
+        if v != ABI_VERSION:
+            raise RuntimeError(f"eraft_amd: libecorr ABI {v} != expected {ABI_VERSION}")
+        _lib = L
+    return _lib
+
+
+def strerror(status: int) -> str:
+    return lib().ecorr_strerror(status).decode()
+
+
+def check(status: int, what: str):
+    if status == ECORR_OK:
+        return
+    msg = f"{what}: {strerror(status)}"
+    if status in (ECORR_EINVAL, ECORR_ERADIUS, ECORR_ELEVELS):
+        raise ValueError(msg)
+    raise RuntimeError(msg)
+
+
+def layout(rows: int, H: int, W: int, levels: int):
+    """(h[], w[], off[]) of the pyramid; raises like avg_pool2d on a 0-pixel level."""
+    h = (_i * levels)()
+    w = (_i * levels)()
+    off = (_i64 * (levels + 1))()
+    check(lib().ecorr_pyramid_layout(rows, H, W, levels, h, w, off), "CorrBlock pyramid")
+    return list(h), list(w), list(off)
+
+
+def stream_of(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)

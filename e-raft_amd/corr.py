@@ -1,0 +1,92 @@
+"""Drop-in CorrBlock for E-RAFT on MI355X (mirrors /root/reference/model/corr.py).
+
+Same constructor and call signatures as the reference:
+    corr_fn = CorrBlock(fmap1, fmap2, num_levels=4, radius=4)      # corr.py:13  (eraft.py:107)
+    corr    = corr_fn(coords1)                                       # corr.py:29  (eraft.py:128)
+    CorrBlock.corr(fmap1, fmap2) -> [B, H, W, 1, H, W]               # corr.py:52
+    corr_fn.corr_pyramid[i] : [B*H*W, 1, h_i, w_i]                   # corr.py:16,24,27
+The work happens in libecorr.so (hand-written gfx950 HIP kernels, C ABI include/ecorr.h): one
+MFMA GEMM launch builds all 4 pyramid levels, one gather launch serves each lookup.  No ATen
+compute op runs on the hot path and there is no CPU fallback.
+
+Contract differences, all loud: inputs must be fp32 HIP tensors (the reference path is fp32,
+eraft.py:104-105); the block is forward-only (E-RAFT only ever calls it under torch.no_grad(),
+test.py:80) and refuses inputs that require grad while grad mode is on; coords must match the
+build's (B, 2, H, W) exactly.
+"""
+import torch
+
+from . import _lib
+
+
+def _require_device_f32(name, t):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name} is on {t.device}: eraft_amd runs only on HIP devices (no CPU path)")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {t.dtype})")
+
+
+def _no_grad_inputs(*ts):
+    if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
+        raise RuntimeError("eraft_amd CorrBlock is forward-only; call it under torch.no_grad() "
+                           "(as the reference harness does, test.py:80)")
+
+
+class CorrBlock:
+    """All-pairs correlation pyramid + radius-r lookup (reference: model/corr.py:12-60)."""
+
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4):
+        self.num_levels = num_levels
+        self.radius = radius
+        _require_device_f32("fmap1", fmap1)
+        _require_device_f32("fmap2", fmap2)
+        _no_grad_inputs(fmap1, fmap2)
+        if fmap1.dim() != 4 or fmap1.shape != fmap2.shape:
+            raise RuntimeError(f"fmap shapes {tuple(fmap1.shape)} / {tuple(fmap2.shape)} differ "
+                               "or are not [B, D, H, W]")
+        if fmap1.device != fmap2.device:
+            raise RuntimeError("fmap1 and fmap2 are on different devices")
+        if not (fmap1.is_contiguous() and fmap2.is_contiguous()):
+            # the reference .view()s them (corr.py:55-56), which raises on these strides
+            raise RuntimeError("fmap1/fmap2 must be contiguous (reference: view size is not "
+                               "compatible with input tensor's size and stride)")
+        B, D, H, W = fmap1.shape
+        self._shape = (B, D, H, W)
+        self._device = fmap1.device
+        Q = H * W
+        self._h, self._w, self._off = _lib.layout(B * Q, H, W, num_levels)
+        with torch.cuda.device(self._device):
+            self._pyramid = torch.empty(self._off[-1], dtype=torch.float32, device=self._device)
+            _lib.check(_lib.lib().ecorr_build(
+                fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, num_levels, 0, Q,
+                self._pyramid.data_ptr(), _lib.stream_of(fmap1)), "CorrBlock build")
+        self.corr_pyramid = [
+            self._pyramid[self._off[i]:self._off[i + 1]].view(B * Q, 1, self._h[i], self._w[i])
+            for i in range(num_levels)]
+
+    def __call__(self, coords):
+        B, _, H, W = self._shape
+        _require_device_f32("coords", coords)
+        _no_grad_inputs(coords)
+        if tuple(coords.shape) != (B, 2, H, W):
+            raise RuntimeError(f"coords shape {tuple(coords.shape)} != {(B, 2, H, W)} of the pyramid")
+        if coords.device != self._device:
+            raise RuntimeError("coords is on a different device than the pyramid")
+        coords = coords.contiguous()   # the reference accepts any strides (permute + reshape)
+        K = 2 * self.radius + 1
+        C = self.num_levels * K * K
+        with torch.cuda.device(self._device):
+            out = torch.empty((B, C, H, W), dtype=torch.float32, device=self._device)
+            _lib.check(_lib.lib().ecorr_lookup(
+                self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, self.num_levels,
+                self.radius, 0, H * W, out.data_ptr(), _lib.stream_of(coords)), "CorrBlock lookup")
+        return out
+
+    @staticmethod
+    def corr(fmap1, fmap2):
+        """Level-0 volume fmap1^T fmap2 / sqrt(D) as [B, H, W, 1, H, W] (corr.py:52-60)."""
+        blk = CorrBlock(fmap1, fmap2, num_levels=1, radius=0)
+        B, _, H, W = fmap1.shape
+        return blk._pyramid.view(B, H, W, 1, H, W)

@@ -1,0 +1,121 @@
+// abi.hip -- extern "C" entry points of libecorr.so (declared in include/ecorr.h).
+//
+// Validation mirrors the reference's failure behaviour where it has one (a pyramid level of zero
+// pixels raises in avg_pool2d, corr.py:26) and rejects what the C ABI cannot express; nothing
+// throws across the boundary.
+#include <math.h>
+
+#include "ecorr_internal.h"
+
+#define ECORR_EXPORT extern "C" __attribute__((visibility("default")))
+
+using namespace ecorr;
+
+namespace {
+
+int layout(int64_t rows, int H, int W, int levels, int* h, int* w, int64_t* off) {
+    if (rows <= 0 || H <= 0 || W <= 0) return ECORR_EINVAL;
+    if (levels < 1 || levels > ECORR_MAX_LEVELS) return ECORR_ELEVELS;
+    int hh = H, ww = W;
+    int64_t o = 0;
+    for (int i = 0; i < levels; ++i) {
+        if (i > 0) { hh /= 2; ww /= 2; }
+        if (hh == 0 || ww == 0) return ECORR_ESHAPE;
+        if (h) h[i] = hh;
+        if (w) w[i] = ww;
+        if (off) off[i] = o;
+        o += rows * hh * ww;
+    }
+    if (off) off[levels] = o;
+    return ECORR_OK;
+}
+
+bool q_range_ok(int H, int W, int q_begin, int q_count) {
+    const int64_t Q = (int64_t)H * W;
+    return Q <= 0x7fffffff && q_begin >= 0 && q_count > 0 && (int64_t)q_begin + q_count <= Q;
+}
+
+}  // namespace
+
+ECORR_EXPORT int ecorr_abi_version(void) { return ECORR_ABI_VERSION; }
+
+ECORR_EXPORT const char* ecorr_strerror(int status) {
+    switch (status) {
+        case ECORR_OK: return "ok";
+        case ECORR_EINVAL: return "invalid argument (null pointer, non-positive size or query range outside [0, H*W])";
+        case ECORR_ESHAPE: return "Output size is too small (a pyramid level would be 0 pixels tall or wide)";
+        case ECORR_ERADIUS: return "radius out of range [0, 32]";
+        case ECORR_ELEVELS: return "num_levels out of range [1, 16]";
+        default: break;
+    }
+    if (status <= ECORR_EHIP) return hipGetErrorString((hipError_t)(ECORR_EHIP - status));
+    return "unknown ecorr status";
+}
+
+ECORR_EXPORT int ecorr_pyramid_layout(int64_t rows, int H, int W, int levels, int* h, int* w, int64_t* off) {
+    return layout(rows, H, W, levels, h, w, off);
+}
+
+ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int levels,
+                             int q_begin, int q_count, float* pyramid, void* stream) {
+    if (!fmap1 || !fmap2 || !pyramid || B <= 0 || D <= 0) return ECORR_EINVAL;
+    if (!q_range_ok(H, W, q_begin, q_count)) return ECORR_EINVAL;
+    int h[ECORR_MAX_LEVELS], w[ECORR_MAX_LEVELS];
+    int64_t off[ECORR_MAX_LEVELS + 1];
+    const int st = layout((int64_t)B * q_count, H, W, levels, h, w, off);
+    if (st != ECORR_OK) return st;
+    float* lvl[ECORR_MAX_LEVELS];
+    for (int i = 0; i < levels; ++i) lvl[i] = pyramid + off[i];
+
+    BuildParams P{};
+    P.f1 = fmap1;
+    P.f2 = fmap2;
+    P.D = D;
+    P.H = H;
+    P.W = W;
+    P.q_begin = q_begin;
+    P.q_count = q_count;
+    // corr.py:60 divides by torch.sqrt(torch.tensor(dim).float()) (IEEE sqrtf).  When that is a
+    // power of two the division is an exact scaling and is done as a multiply.
+    const float s = sqrtf((float)D);
+    int e = 0;
+    const float mant = frexpf(s, &e);
+    P.scale_is_mul = (mant == 0.5f) ? 1 : 0;
+    P.scale = P.scale_is_mul ? 1.0f / s : s;
+    return launch_build(P, B, levels, h, w, lvl, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int levels,
+                              int radius, int q_begin, int q_count, float* out, void* stream) {
+    if (!pyramid || !coords || !out || B <= 0) return ECORR_EINVAL;
+    if (!q_range_ok(H, W, q_begin, q_count)) return ECORR_EINVAL;
+    if (radius < 0 || radius > 32) return ECORR_ERADIUS;
+    LookupParams P{};
+    int64_t off[ECORR_MAX_LEVELS + 1];
+    const int st = layout((int64_t)B * q_count, H, W, levels, P.lh, P.lw, off);
+    if (st != ECORR_OK) return st;
+    for (int i = 0; i < levels; ++i) P.lvl[i] = pyramid + off[i];
+    P.coords = coords;
+    P.out = out;
+    P.H = H;
+    P.W = W;
+    P.q_begin = q_begin;
+    P.q_count = q_count;
+    P.levels = levels;
+    P.radius = radius;
+    P.C = levels * (2 * radius + 1) * (2 * radius + 1);
+    if ((int64_t)B * P.C > 0xffff * 64) return ECORR_EINVAL;
+    return launch_lookup(P, B, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,
+                                        int Hg, int Wg, float* out, float* mask, void* stream) {
+    if (!img || !coords || !out || N <= 0 || C < 0 || h <= 0 || w <= 0 || Hg <= 0 || Wg <= 0)
+        return ECORR_EINVAL;
+    return launch_bilinear_sampler(img, N, C, h, w, coords, Hg, Wg, out, mask, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_coords_grid(int B, int H, int W, float* out, void* stream) {
+    if (!out || B <= 0 || H <= 0 || W <= 0) return ECORR_EINVAL;
+    return launch_coords_grid(B, H, W, out, (hipStream_t)stream);
+}

@@ -1,0 +1,54 @@
+// ecorr_device.h -- device helpers shared by the build and lookup kernels (gfx950 only).
+//
+// Exactness contract: every helper below performs the reference's fp32 operations in the
+// reference's order with explicit round-to-nearest intrinsics, so no -ffp-contract setting or
+// compiler reassociation can change a bit.  The library is additionally compiled with
+// -ffp-contract=off.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ecorr {
+
+constexpr int kWave = 64;
+
+// model/utils.py:11-12 then ATen grid_sampler unnormalize (align_corners=True):
+//   g  = RN(RN(2x / (size-1)) - 1)
+//   ix = RN(RN(g + 1) * ((size-1)/2))
+// 2x and (size-1)/2 are exact; the division is IEEE (v_div_scale/fmas/fixup sequence).
+__device__ __forceinline__ float unnormalize(float x, float size_m1, float half_size_m1) {
+    const float g = __fsub_rn(__fdiv_rn(__fmul_rn(2.0f, x), size_m1), 1.0f);
+    return __fmul_rn(__fadd_rn(g, 1.0f), half_size_m1);
+}
+
+// Bilinear blend exactly as ATen's AVX512 grid_sampler (nw product, then FMA chain).
+// w = x-frac, n = y-frac; out-of-image corners must already be 0.
+__device__ __forceinline__ float blend(float vnw, float vne, float vsw, float vse, float w, float n) {
+    const float e = __fsub_rn(1.0f, w);
+    const float s = __fsub_rn(1.0f, n);
+    float acc = __fmul_rn(vnw, __fmul_rn(s, e));
+    acc = __builtin_fmaf(vne, __fmul_rn(s, w), acc);
+    acc = __builtin_fmaf(vsw, __fmul_rn(n, e), acc);
+    acc = __builtin_fmaf(vse, __fmul_rn(n, w), acc);
+    return acc;
+}
+
+// Zeros-padding corner fetch by float coordinates (float compare: NaN and +-huge read 0, exactly
+// as ATen's int32-converted masks do).  Used by the generic / fallback paths only.
+__device__ __forceinline__ float corner(const float* __restrict__ img, int h, int w, float fx, float fy) {
+    const bool in = (fx >= 0.0f) & (fx < (float)w) & (fy >= 0.0f) & (fy < (float)h);
+    return in ? img[(int64_t)(int)fy * w + (int)fx] : 0.0f;
+}
+
+// One bilinear sample of img[h][w] at pixel coordinates (x, y) (model/utils.py:7-21).
+__device__ __forceinline__ float sample_px(const float* __restrict__ img, int h, int w, float x, float y) {
+    const float ix = unnormalize(x, (float)(w - 1), (float)(w - 1) * 0.5f);
+    const float iy = unnormalize(y, (float)(h - 1), (float)(h - 1) * 0.5f);
+    const float x0 = floorf(ix), y0 = floorf(iy);
+    const float wx = __fsub_rn(ix, x0), wy = __fsub_rn(iy, y0);
+    const float x1 = __fadd_rn(x0, 1.0f), y1 = __fadd_rn(y0, 1.0f);
+    return blend(corner(img, h, w, x0, y0), corner(img, h, w, x1, y0), corner(img, h, w, x0, y1),
+                 corner(img, h, w, x1, y1), wx, wy);
+}
+
+}  // namespace ecorr

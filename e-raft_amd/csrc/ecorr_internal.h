@@ -1,0 +1,45 @@
+// ecorr_internal.h -- host-side launch interfaces between abi.hip and the kernel files.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ecorr.h"
+
+namespace ecorr {
+
+struct BuildParams {
+    const float* f1;
+    const float* f2;
+    int D, H, W;
+    int q_begin, q_count;
+    float scale;        // sqrt(D) (divide) or 1/sqrt(D) when sqrt(D) is a power of two (multiply)
+    int scale_is_mul;
+    // filled by launch_build
+    int n_mt, n_nt, n_ntx;
+    int fused_levels;   // levels written by the GEMM epilogue (<= 4)
+    float* lvl[4];
+    int lh[4], lw[4];
+};
+
+int launch_build(const BuildParams& P, int B, int levels, const int* lh, const int* lw,
+                 float* const* lvl, hipStream_t stream);
+
+struct LookupParams {
+    const float* coords;  // [B][2][H][W]
+    float* out;           // [B][C][q_count]
+    int H, W;
+    int q_begin, q_count;
+    int levels, radius;
+    int C;                // levels * (2r+1)^2
+    const float* lvl[ECORR_MAX_LEVELS];
+    int lh[ECORR_MAX_LEVELS], lw[ECORR_MAX_LEVELS];
+};
+
+int launch_lookup(const LookupParams& P, int B, hipStream_t stream);
+
+int launch_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,
+                            int Hg, int Wg, float* out, float* mask, hipStream_t stream);
+
+int launch_coords_grid(int B, int H, int W, float* out, hipStream_t stream);
+
+}  // namespace ecorr

@@ -1,0 +1,79 @@
+/*
+ * ecorr.h -- C ABI of the MI355X-native E-RAFT correlation hot path (libecorr.so, gfx950).
+ *
+ * Drop-in boundary for wzygzlm/E-RAFT's model/corr.py CorrBlock and the model/utils.py helpers.
+ * Every entry point is stream-ordered and asynchronous on `stream` (a hipStream_t passed as
+ * void*, e.g. torch.cuda.current_stream().cuda_stream); all buffers are device pointers owned by
+ * the caller (PyTorch's caching allocator); the library allocates nothing and keeps no global
+ * mutable state.  Return value: ECORR_OK (0) or a negative code; ecorr_strerror() names it.  No
+ * C++ exception crosses this boundary.
+ *
+ * Pyramid storage (what ecorr_build writes, ecorr_lookup reads): `levels` blocks concatenated,
+ * level i = float[rows][h_i][w_i] at float offset off_i, rows = B * q_count, h_0 = H, w_0 = W,
+ * h_{i+1} = h_i / 2, w_{i+1} = w_i / 2 (floor) -- exactly the reference's corr_pyramid[i]
+ * ([B*H*W, 1, h_i, w_i], corr.py:16-27), so level i is a zero-copy view for the Python shim.
+ *
+ * Query-row sharding (multi-GPU): q_begin/q_count select a contiguous range of query
+ * pixels p = y*W + x of every batch item; the unsharded call is q_begin = 0, q_count = H*W.
+ */
+#ifndef ECORR_H
+#define ECORR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ECORR_ABI_VERSION 1
+#define ECORR_MAX_LEVELS 16
+
+enum ecorr_status {
+    ECORR_OK = 0,
+    ECORR_EINVAL = -1,   /* null pointer, non-positive size, q range outside [0, H*W] */
+    ECORR_ESHAPE = -2,   /* a pyramid level would be 0 pixels tall or wide (reference: avg_pool2d
+                            raises "Output size is too small", corr.py:26) */
+    ECORR_ERADIUS = -3,  /* radius < 0 or > 32 */
+    ECORR_ELEVELS = -4,  /* levels < 1 or > ECORR_MAX_LEVELS */
+    ECORR_EHIP = -1000   /* HIP error e is reported as ECORR_EHIP - e */
+};
+
+/* Layout of the pyramid for `rows` query rows (rows = B * q_count).  Writes h[levels],
+ * w[levels], off[levels + 1] (float offsets; off[levels] = total floats).
+ * Replaces: the shapes produced by CorrBlock.__init__'s reshape + avg_pool2d loop, corr.py:21-27. */
+int ecorr_pyramid_layout(int64_t rows, int H, int W, int levels, int* h, int* w, int64_t* off);
+
+/* Build the correlation pyramid: level 0 = fmap1^T fmap2 / sqrt(D) over the query range, levels
+ * 1.. = 2x2 floor-mode average pools.  fmap1, fmap2: float[B][D][H][W] contiguous.
+ * Replaces: CorrBlock.__init__ (corr.py:13-27) and CorrBlock.corr (corr.py:52-60). */
+int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int levels,
+                int q_begin, int q_count, float* pyramid, void* stream);
+
+/* Radius-r lookup: out[B][levels*(2r+1)^2][q_count] (= [B][C][H][W] when unsharded), channel
+ * 81*i + 9*a + b (r = 4) = bilinear sample of level i at (x/2^i + a - r, y/2^i + b - r), zeros
+ * padding.  coords: float[B][2][H][W] contiguous (channel 0 = x, 1 = y); only queries
+ * [q_begin, q_begin + q_count) are read.  Bit-exact with the reference on CPU.
+ * Replaces: CorrBlock.__call__ (corr.py:29-50) incl. bilinear_sampler (utils.py:7-21). */
+int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int levels,
+                 int radius, int q_begin, int q_count, float* out, void* stream);
+
+/* Generic bilinear_sampler: img float[N][C][h][w], coords float[N][Hg][Wg][2] in pixels ->
+ * out float[N][C][Hg][Wg]; mask (nullable) float[N][Hg][Wg] = 1 where the normalized sample
+ * lies strictly inside (-1, 1)^2.  Replaces: model/utils.py:7-21. */
+int ecorr_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,
+                           int Hg, int Wg, float* out, float* mask, void* stream);
+
+/* coords_grid: out float[B][2][H][W], channel 0 = x (column), 1 = y (row).
+ * Replaces: model/utils.py:24-27. */
+int ecorr_coords_grid(int B, int H, int W, float* out, void* stream);
+
+/* Human-readable name of a status code (static storage). */
+const char* ecorr_strerror(int status);
+
+/* ECORR_ABI_VERSION of the loaded library. */
+int ecorr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ECORR_H */

@@ -1,0 +1,46 @@
+"""torch-CPU restatement of the reference CorrBlock -- the CPU baseline ("port") that bench.py times.
+
+TEST/BASELINE INFRASTRUCTURE ONLY (see oracle/ecorr_oracle.c header): the reference Python cannot
+travel to the GPU box, so bench.py's cpu_baseline leg times this restatement instead.  It issues
+the same ATen ops as /root/reference/model/corr.py and model/utils.py, in the same order:
+  build:  bmm(f1^T, f2) -> div by sqrt(D) (corr.py:52-60) -> 3 x avg_pool2d(2, 2) (corr.py:25-27)
+  lookup: per level, CPU-built offset grid, coords / 2**i + offsets, pixel -> [-1, 1] mapping,
+          grid_sample(align_corners=True) (utils.py:7-21), then cat + permute + contiguous
+          (corr.py:35-50).
+tests/test_torch_ref.py checks it bit-for-bit against the golden fixtures.
+"""
+import torch
+import torch.nn.functional as F
+
+
+class TorchCpuCorrBlock:
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4):
+        self.num_levels, self.radius = num_levels, radius
+        B, D, H, W = fmap1.shape
+        a = fmap1.reshape(B, D, H * W).transpose(1, 2)
+        vol = torch.bmm(a, fmap2.reshape(B, D, H * W))
+        vol = vol / torch.sqrt(torch.tensor(D, dtype=torch.float32))
+        lvl = vol.reshape(B * H * W, 1, H, W)
+        self.corr_pyramid = [lvl]
+        for _ in range(num_levels - 1):
+            lvl = F.avg_pool2d(lvl, 2, stride=2)
+            self.corr_pyramid.append(lvl)
+
+    def __call__(self, coords):
+        r = self.radius
+        B, _, H, W = coords.shape
+        c = coords.permute(0, 2, 3, 1).reshape(B * H * W, 1, 1, 2)
+        k = 2 * r + 1
+        steps = torch.linspace(-r, r, k)
+        oy, ox = torch.meshgrid(steps, steps, indexing="ij")
+        # last axis = (first meshgrid output, second) as in corr.py:39
+        offs = torch.stack([oy, ox], dim=-1).view(1, k, k, 2)
+        outs = []
+        for i, img in enumerate(self.corr_pyramid):
+            pts = c / 2 ** i + offs
+            h, w = img.shape[-2:]
+            px, py = pts[..., :1], pts[..., 1:]
+            grid = torch.cat([2 * px / (w - 1) - 1, 2 * py / (h - 1) - 1], dim=-1)
+            s = F.grid_sample(img, grid, align_corners=True)
+            outs.append(s.view(B, H, W, -1))
+        return torch.cat(outs, dim=-1).permute(0, 3, 1, 2).contiguous().float()

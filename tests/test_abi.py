@@ -1,0 +1,81 @@
+"""CPU-side checks of the C ABI: the library builds for gfx950, loads, exports every symbol the
+header declares, and validates arguments before touching a device (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "ecorr.h")
+
+
+def _declared():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ecorr_\w+)\s*\(", txt, re.M)))
+
+
+@pytest.fixture(scope="module")
+def ea():
+    lib = os.path.join(ROOT, "e-raft_amd", "libecorr.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "e-raft_amd", "csrc")], check=True)
+    import eraft_amd
+    eraft_amd.lib()
+    return eraft_amd
+
+
+def test_header_symbols_exported(ea):
+    names = _declared()
+    assert {"ecorr_build", "ecorr_lookup", "ecorr_pyramid_layout", "ecorr_bilinear_sampler",
+            "ecorr_coords_grid", "ecorr_strerror", "ecorr_abi_version"} <= set(names)
+    L = ctypes.CDLL(ea.LIB_PATH)
+    for n in names:
+        assert hasattr(L, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", ea.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (ecorr_\w+)", out))
+    assert exported == set(names)
+
+
+def test_code_object_is_gfx950(ea):
+    # the embedded HIP fat binary names its offload targets (amdgcn-amd-amdhsa--gfx950)
+    data = open(ea.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa-+(gfx\w+)", data))
+    assert targets == {b"gfx950"}
+
+
+def test_layout_matches_reference_shapes(ea):
+    from eraft_amd import _lib
+    h, w, off = _lib.layout(16 * 4800, 60, 80, 4)
+    assert (h, w) == ([60, 30, 15, 7], [80, 40, 20, 10])
+    assert off == [0, 368640000, 460800000, 483840000, 489216000]
+    h, w, _ = _lib.layout(396, 18, 22, 4)
+    assert (h, w) == ([18, 9, 4, 2], [22, 11, 5, 2])
+
+
+@pytest.mark.parametrize("hw", [(4, 4), (2, 40), (6, 6)])
+def test_zero_level_raises_like_reference(ea, hw):
+    from eraft_amd import _lib
+    with pytest.raises(RuntimeError, match="too small"):
+        _lib.layout(hw[0] * hw[1], hw[0], hw[1], 4)
+
+
+def test_argument_validation_before_launch(ea):
+    L = ea.lib()
+    from eraft_amd import _lib
+    assert L.ecorr_build(None, None, 1, 256, 8, 8, 4, 0, 64, None, None) == _lib.ECORR_EINVAL
+    # query range outside [0, H*W]
+    assert L.ecorr_build(8, 8, 1, 256, 8, 8, 4, 60, 8, 8, None) == _lib.ECORR_EINVAL
+    assert L.ecorr_lookup(8, 8, 1, 8, 8, 4, 33, 0, 64, 8, None) == _lib.ECORR_ERADIUS
+    assert L.ecorr_lookup(8, 8, 1, 8, 8, 0, 4, 0, 64, 8, None) == _lib.ECORR_ELEVELS
+    assert L.ecorr_lookup(8, 8, 1, 4, 4, 4, 4, 0, 16, 8, None) == _lib.ECORR_ESHAPE
+    assert "too small" in _lib.strerror(_lib.ECORR_ESHAPE)
+
+
+def test_cpu_tensors_rejected_loudly(ea):
+    import torch
+    f = torch.zeros(1, 16, 8, 8)
+    with pytest.raises(RuntimeError, match="HIP"):
+        ea.CorrBlock(f, f)

@@ -1,0 +1,28 @@
+"""Pin the torch-CPU restatement (bench.py's cpu_baseline) bit-for-bit to the reference goldens."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import prng
+from conftest import GOLDEN
+from torch_ref import TorchCpuCorrBlock
+
+CASES = sorted(glob.glob(os.path.join(GOLDEN, "corr_*.npz")))
+
+
+@pytest.mark.parametrize("path", CASES, ids=lambda p: os.path.basename(p)[:-4])
+def test_torch_ref_matches_reference(path):
+    z = np.load(path)
+    B, D, H, W, L, r, seed = (int(z[k]) for k in ("B", "D", "H", "W", "L", "r", "seed"))
+    f1, f2 = prng.normal(seed, (B, D, H, W)), prng.normal(seed + 1, (B, D, H, W))
+    blk = TorchCpuCorrBlock(torch.from_numpy(f1), torch.from_numpy(f2), num_levels=L, radius=r)
+    for i in range(L):   # same ATen sgemm as the reference on this host -> identical bits
+        assert oracle.same_bits(blk.corr_pyramid[i][:, 0].numpy(), z[f"level{i}"])
+    for k in z.files:
+        if k.startswith("coords_"):
+            s = k[len("coords_"):]
+            assert oracle.same_bits(blk(torch.from_numpy(z[k])).numpy(), z[f"out_{s}"]), s
