@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -34,8 +34,10 @@ SYMBOLS = {
     "ecorr_strerror": (ctypes.c_char_p, [_i]),
     "ecorr_pyramid_layout": (_i, [_i64, _i, _i, _i, ctypes.POINTER(_i), ctypes.POINTER(_i),
                                   ctypes.POINTER(_i64)]),
-    "ecorr_build": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
-    "ecorr_lookup": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
+    # (fmap1, fmap2, B, D, H, W, q_count, levels, pyramid, stream)
+    "ecorr_build": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
+    # (pyramid, coords, B, H, W, q_count, levels, radius, out, stream)
+    "ecorr_lookup": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
     "ecorr_bilinear_sampler": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _p]),
     "ecorr_coords_grid": (_i, [_i, _i, _i, _p, _p]),
 }

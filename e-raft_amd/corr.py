@@ -60,7 +60,7 @@ class CorrBlock:
         with torch.cuda.device(self._device):
             self._pyramid = torch.empty(self._off[-1], dtype=torch.float32, device=self._device)
             _lib.check(_lib.lib().ecorr_build(
-                fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, num_levels, 0, Q,
+                fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, Q, num_levels,
                 self._pyramid.data_ptr(), _lib.stream_of(fmap1)), "CorrBlock build")
         self.corr_pyramid = [
             self._pyramid[self._off[i]:self._off[i + 1]].view(B * Q, 1, self._h[i], self._w[i])
@@ -80,8 +80,8 @@ class CorrBlock:
         with torch.cuda.device(self._device):
             out = torch.empty((B, C, H, W), dtype=torch.float32, device=self._device)
             _lib.check(_lib.lib().ecorr_lookup(
-                self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, self.num_levels,
-                self.radius, 0, H * W, out.data_ptr(), _lib.stream_of(coords)), "CorrBlock lookup")
+                self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, self.num_levels,
+                self.radius, out.data_ptr(), _lib.stream_of(coords)), "CorrBlock lookup")
         return out
 
     @staticmethod

@@ -30,9 +30,9 @@ int layout(int64_t rows, int H, int W, int levels, int* h, int* w, int64_t* off)
     return ECORR_OK;
 }
 
-bool q_range_ok(int H, int W, int q_begin, int q_count) {
+bool q_count_ok(int H, int W, int q_count) {
     const int64_t Q = (int64_t)H * W;
-    return Q <= 0x7fffffff && q_begin >= 0 && q_count > 0 && (int64_t)q_begin + q_count <= Q;
+    return H > 0 && W > 0 && Q <= 0x7fffffff && q_count > 0 && q_count <= Q;
 }
 
 }  // namespace
@@ -42,7 +42,7 @@ ECORR_EXPORT int ecorr_abi_version(void) { return ECORR_ABI_VERSION; }
 ECORR_EXPORT const char* ecorr_strerror(int status) {
     switch (status) {
         case ECORR_OK: return "ok";
-        case ECORR_EINVAL: return "invalid argument (null pointer, non-positive size or query range outside [0, H*W])";
+        case ECORR_EINVAL: return "invalid argument (null pointer, non-positive size or q_count outside [1, H*W])";
         case ECORR_ESHAPE: return "Output size is too small (a pyramid level would be 0 pixels tall or wide)";
         case ECORR_ERADIUS: return "radius out of range [0, 32]";
         case ECORR_ELEVELS: return "num_levels out of range [1, 16]";
@@ -56,10 +56,10 @@ ECORR_EXPORT int ecorr_pyramid_layout(int64_t rows, int H, int W, int levels, in
     return layout(rows, H, W, levels, h, w, off);
 }
 
-ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int levels,
-                             int q_begin, int q_count, float* pyramid, void* stream) {
+ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
+                             int levels, float* pyramid, void* stream) {
     if (!fmap1 || !fmap2 || !pyramid || B <= 0 || D <= 0) return ECORR_EINVAL;
-    if (!q_range_ok(H, W, q_begin, q_count)) return ECORR_EINVAL;
+    if (!q_count_ok(H, W, q_count)) return ECORR_EINVAL;
     int h[ECORR_MAX_LEVELS], w[ECORR_MAX_LEVELS];
     int64_t off[ECORR_MAX_LEVELS + 1];
     const int st = layout((int64_t)B * q_count, H, W, levels, h, w, off);
@@ -73,7 +73,6 @@ ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int 
     P.D = D;
     P.H = H;
     P.W = W;
-    P.q_begin = q_begin;
     P.q_count = q_count;
     // corr.py:60 divides by torch.sqrt(torch.tensor(dim).float()) (IEEE sqrtf).  When that is a
     // power of two the division is an exact scaling and is done as a multiply.
@@ -85,10 +84,10 @@ ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int 
     return launch_build(P, B, levels, h, w, lvl, (hipStream_t)stream);
 }
 
-ECORR_EXPORT int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int levels,
-                              int radius, int q_begin, int q_count, float* out, void* stream) {
+ECORR_EXPORT int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
+                              int levels, int radius, float* out, void* stream) {
     if (!pyramid || !coords || !out || B <= 0) return ECORR_EINVAL;
-    if (!q_range_ok(H, W, q_begin, q_count)) return ECORR_EINVAL;
+    if (!q_count_ok(H, W, q_count)) return ECORR_EINVAL;
     if (radius < 0 || radius > 32) return ECORR_ERADIUS;
     LookupParams P{};
     int64_t off[ECORR_MAX_LEVELS + 1];
@@ -99,7 +98,6 @@ ECORR_EXPORT int ecorr_lookup(const float* pyramid, const float* coords, int B, 
     P.out = out;
     P.H = H;
     P.W = W;
-    P.q_begin = q_begin;
     P.q_count = q_count;
     P.levels = levels;
     P.radius = radius;

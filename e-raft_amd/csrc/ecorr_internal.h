@@ -11,12 +11,14 @@ struct BuildParams {
     const float* f1;
     const float* f2;
     int D, H, W;
-    int q_begin, q_count;
+    int q_count;        // query pixels in the fmap1 slab
     float scale;        // sqrt(D) (divide) or 1/sqrt(D) when sqrt(D) is a power of two (multiply)
     int scale_is_mul;
     // filled by launch_build
-    int n_mt, n_nt, n_ntx;
+    int n_mt, n_nt, n_ntx, n_tiles;
     int fused_levels;   // levels written by the GEMM epilogue (<= 4)
+    int dev_skip_epilogue;  // A/B ablation only (ECORR_BUILD_SKIP_EPILOGUE): no pyramid stores
+    int dev_epilogue_v2;    // A/B only (ECORR_BUILD_OLD_EPILOGUE): per-thread scattered stores
     float* lvl[4];
     int lh[4], lw[4];
 };
@@ -25,10 +27,10 @@ int launch_build(const BuildParams& P, int B, int levels, const int* lh, const i
                  float* const* lvl, hipStream_t stream);
 
 struct LookupParams {
-    const float* coords;  // [B][2][H][W]
+    const float* coords;  // [B][2][q_count]
     float* out;           // [B][C][q_count]
     int H, W;
-    int q_begin, q_count;
+    int q_count;
     int levels, radius;
     int C;                // levels * (2r+1)^2
     const float* lvl[ECORR_MAX_LEVELS];

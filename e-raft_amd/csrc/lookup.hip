@@ -41,10 +41,10 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
     const int tid = threadIdx.x, g = tid & (QB - 1), part = tid >> 6;
     const int lv = blockIdx.y, b = blockIdx.z;
     const int h = P.lh[lv], w = P.lw[lv];
-    const int q0 = blockIdx.x * QB;                 // first query of the block, relative
-    const int p = P.q_begin + q0 + g;               // query pixel index within the batch item
-    const bool valid = q0 + g < P.q_count;
-    const int64_t Q = (int64_t)P.H * P.W;
+    const int q0 = blockIdx.x * QB;                 // first query of the block (in the slab)
+    const int p = q0 + g;
+    const bool valid = p < P.q_count;
+    const int64_t Q = P.q_count;                    // coords slab stride
     const int64_t hw = (int64_t)h * w;
     const float* __restrict__ lvbase = P.lvl[lv] + ((int64_t)b * P.q_count + q0) * hw;
 
@@ -89,21 +89,41 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
     }
     __syncthreads();
 
-    // ---- phase 1: stage windows, zeros outside the image (grid_sample padding_mode='zeros')
-    for (int f = tid; f < QB * SS; f += NT) {
-        const int gq = f / SS;
-        const int r = f - gq * SS;
-        const int ry = r / S, rx = r - ry * S;
-        float val = 0.0f;
-        if (mode[gq] == 0) {
-            const int y = org[gq][1] + ry, x = org[gq][0] + rx;
-            const bool in = ((unsigned)y < (unsigned)h) & ((unsigned)x < (unsigned)w);
-            const int yc = min(max(y, 0), h - 1), xc = min(max(x, 0), w - 1);
-            const float t = lvbase[(int64_t)gq * hw + (int64_t)yc * w + xc];
-            val = in ? t : 0.0f;
+    // ---- phase 1: stage windows, zeros outside the image (grid_sample padding_mode='zeros').
+    // Work item = (query, window column); each item walks the S rows.  Loads are raw buffer loads
+    // over this block's slab of the level: an element outside the image gets an out-of-range
+    // offset and the hardware range check returns 0 -- zero padding with no branch and no select,
+    // so all NCOL*S loads of a thread issue back to back.
+    constexpr int ITEMS = QB * S;
+    constexpr int NCOL = (ITEMS + NT - 1) / NT;
+    const int nq = min(QB, P.q_count - q0);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lvbase), 0, (int)(nq * hw * 4), 0x00020000);
+    constexpr int OOB = 0x7ffffff0;   // beyond any slab: reads as 0
+    float vals[NCOL][S];
+    int dst[NCOL];
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) {
+        const int it = tid + c * NT;
+        const bool live = it < ITEMS;
+        const int gq = live ? it / S : 0;
+        const int rx = it - gq * S;
+        const int x = org[gq][0] + rx, y0 = org[gq][1];
+        const bool colin = live && mode[gq] == 0 && (unsigned)x < (unsigned)w;
+        const int base = (int)(gq * hw) + x;
+        dst[c] = live ? gq * SP + rx : -1;
+#pragma unroll
+        for (int ry = 0; ry < S; ++ry) {
+            const int y = y0 + ry;
+            const int off = (colin && (unsigned)y < (unsigned)h) ? (base + y * w) * 4 : OOB;
+            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
         }
-        win[gq * SP + r] = val;
     }
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c)
+        if (dst[c] >= 0)
+#pragma unroll
+            for (int ry = 0; ry < S; ++ry) win[dst[c] + ry * S] = vals[c][ry];
     __syncthreads();
 
     // ---- phase 2: outputs; lanes = queries -> coalesced channel-row stores
@@ -135,14 +155,14 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
 __global__ __launch_bounds__(NT) void lookup_direct(LookupParams P, int B) {
     const int K = 2 * P.radius + 1, KK = K * K;
     const int64_t n = (int64_t)B * P.C * P.q_count;
-    const int64_t Q = (int64_t)P.H * P.W;
+    const int64_t Q = P.q_count;
     for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
         const int64_t bc = i / P.q_count;
         const int qq = (int)(i - bc * P.q_count);
         const int b = (int)(bc / P.C), ch = (int)(bc - (int64_t)b * P.C);
         const int lv = ch / KK, k = ch - lv * KK, a = k / K, bb = k - a * K;
         const int h = P.lh[lv], w = P.lw[lv];
-        const int p = P.q_begin + qq;
+        const int p = qq;
         const float inv = 1.0f / (float)(1 << lv);
         const float cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
         const float cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);

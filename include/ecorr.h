@@ -13,8 +13,9 @@
  * h_{i+1} = h_i / 2, w_{i+1} = w_i / 2 (floor) -- exactly the reference's corr_pyramid[i]
  * ([B*H*W, 1, h_i, w_i], corr.py:16-27), so level i is a zero-copy view for the Python shim.
  *
- * Query-row sharding (multi-GPU): q_begin/q_count select a contiguous range of query
- * pixels p = y*W + x of every batch item; the unsharded call is q_begin = 0, q_count = H*W.
+ * Query slabs (multi-GPU query-row sharding): fmap1, coords and the lookup output hold
+ * the q_count query pixels being served -- all H*W of them for the plain CorrBlock, a contiguous
+ * block of image rows on a query-row shard.  fmap2 is always the whole [B][D][H][W] target map.
  */
 #ifndef ECORR_H
 #define ECORR_H
@@ -25,12 +26,12 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 1
+#define ECORR_ABI_VERSION 2
 #define ECORR_MAX_LEVELS 16
 
 enum ecorr_status {
     ECORR_OK = 0,
-    ECORR_EINVAL = -1,   /* null pointer, non-positive size, q range outside [0, H*W] */
+    ECORR_EINVAL = -1,   /* null pointer, non-positive size, q_count outside [1, H*W] */
     ECORR_ESHAPE = -2,   /* a pyramid level would be 0 pixels tall or wide (reference: avg_pool2d
                             raises "Output size is too small", corr.py:26) */
     ECORR_ERADIUS = -3,  /* radius < 0 or > 32 */
@@ -43,19 +44,20 @@ enum ecorr_status {
  * Replaces: the shapes produced by CorrBlock.__init__'s reshape + avg_pool2d loop, corr.py:21-27. */
 int ecorr_pyramid_layout(int64_t rows, int H, int W, int levels, int* h, int* w, int64_t* off);
 
-/* Build the correlation pyramid: level 0 = fmap1^T fmap2 / sqrt(D) over the query range, levels
- * 1.. = 2x2 floor-mode average pools.  fmap1, fmap2: float[B][D][H][W] contiguous.
+/* Build the correlation pyramid: level 0 = fmap1^T fmap2 / sqrt(D), levels 1.. = 2x2 floor-mode
+ * average pools.  fmap1: float[B][D][q_count] (the query slab; = [B][D][H][W] when q_count = H*W),
+ * fmap2: float[B][D][H][W], both contiguous.  pyramid: ecorr_pyramid_layout(B*q_count, ...) floats.
  * Replaces: CorrBlock.__init__ (corr.py:13-27) and CorrBlock.corr (corr.py:52-60). */
-int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int levels,
-                int q_begin, int q_count, float* pyramid, void* stream);
+int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
+                int levels, float* pyramid, void* stream);
 
-/* Radius-r lookup: out[B][levels*(2r+1)^2][q_count] (= [B][C][H][W] when unsharded), channel
- * 81*i + 9*a + b (r = 4) = bilinear sample of level i at (x/2^i + a - r, y/2^i + b - r), zeros
- * padding.  coords: float[B][2][H][W] contiguous (channel 0 = x, 1 = y); only queries
- * [q_begin, q_begin + q_count) are read.  Bit-exact with the reference on CPU.
+/* Radius-r lookup: out float[B][levels*(2r+1)^2][q_count] (= [B][C][H][W] when q_count = H*W),
+ * channel 81*i + 9*a + b (r = 4) = bilinear sample of level i at (x/2^i + a - r, y/2^i + b - r),
+ * zeros padding.  coords: float[B][2][q_count] contiguous (channel 0 = x, 1 = y, pixel units of
+ * the H x W map).  Bit-exact with the reference on CPU.
  * Replaces: CorrBlock.__call__ (corr.py:29-50) incl. bilinear_sampler (utils.py:7-21). */
-int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int levels,
-                 int radius, int q_begin, int q_count, float* out, void* stream);
+int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
+                 int levels, int radius, float* out, void* stream);
 
 /* Generic bilinear_sampler: img float[N][C][h][w], coords float[N][Hg][Wg][2] in pixels ->
  * out float[N][C][Hg][Wg]; mask (nullable) float[N][Hg][Wg] = 1 where the normalized sample

@@ -65,12 +65,13 @@ def test_zero_level_raises_like_reference(ea, hw):
 def test_argument_validation_before_launch(ea):
     L = ea.lib()
     from eraft_amd import _lib
-    assert L.ecorr_build(None, None, 1, 256, 8, 8, 4, 0, 64, None, None) == _lib.ECORR_EINVAL
-    # query range outside [0, H*W]
-    assert L.ecorr_build(8, 8, 1, 256, 8, 8, 4, 60, 8, 8, None) == _lib.ECORR_EINVAL
-    assert L.ecorr_lookup(8, 8, 1, 8, 8, 4, 33, 0, 64, 8, None) == _lib.ECORR_ERADIUS
-    assert L.ecorr_lookup(8, 8, 1, 8, 8, 0, 4, 0, 64, 8, None) == _lib.ECORR_ELEVELS
-    assert L.ecorr_lookup(8, 8, 1, 4, 4, 4, 4, 0, 16, 8, None) == _lib.ECORR_ESHAPE
+    assert L.ecorr_build(None, None, 1, 256, 8, 8, 64, 4, None, None) == _lib.ECORR_EINVAL
+    # q_count outside [1, H*W]
+    assert L.ecorr_build(8, 8, 1, 256, 8, 8, 65, 4, 8, None) == _lib.ECORR_EINVAL
+    assert L.ecorr_build(8, 8, 1, 256, 8, 8, 0, 4, 8, None) == _lib.ECORR_EINVAL
+    assert L.ecorr_lookup(8, 8, 1, 8, 8, 64, 4, 33, 8, None) == _lib.ECORR_ERADIUS
+    assert L.ecorr_lookup(8, 8, 1, 8, 8, 64, 0, 4, 8, None) == _lib.ECORR_ELEVELS
+    assert L.ecorr_lookup(8, 8, 1, 4, 4, 16, 4, 4, 8, None) == _lib.ECORR_ESHAPE
     assert "too small" in _lib.strerror(_lib.ECORR_ESHAPE)
 
 

@@ -49,8 +49,8 @@ def _lookup_on(ea, levels, coords, radius):
     c = torch.from_numpy(np.ascontiguousarray(coords)).to(DEV)
     K = 2 * radius + 1
     out = torch.empty((B, len(levels) * K * K, H, W), dtype=torch.float32, device=DEV)
-    _lib.check(_lib.lib().ecorr_lookup(flat.data_ptr(), c.data_ptr(), B, H, W, len(levels), radius, 0,
-                                       H * W, out.data_ptr(), _lib.stream_of(out)), "lookup")
+    _lib.check(_lib.lib().ecorr_lookup(flat.data_ptr(), c.data_ptr(), B, H, W, H * W, len(levels),
+                                       radius, out.data_ptr(), _lib.stream_of(out)), "lookup")
     torch.cuda.synchronize()
     return out.cpu().numpy()
 
