@@ -35,8 +35,10 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
     constexpr int SP = SS | 1;     // odd per-query stride: conflict-free lanes = queries
     __shared__ float win[QB * SP];
     __shared__ float fx[QB][K], wx[QB][K], fy[QB][K], wy[QB][K];
-    __shared__ int org[QB][2];
-    __shared__ int mode[QB];       // 0 staged, 1 direct gather, 2 past the query range
+    // per query: window origin x, y and (mode | needed cols << 8 | needed rows << 16), where mode
+    // 0 = staged, 1 = direct gather (coordinates that do not fit the window), 2 = past the range.
+    // Kept at 40 KB of LDS in total so 4 blocks fit a CU.
+    __shared__ int org[QB][3];
 
     const int tid = threadIdx.x, g = tid & (QB - 1), part = tid >> 6;
     const int lv = blockIdx.y, b = blockIdx.z;
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
 
     // ---- phase 0b: window origin and fast/slow decision per query
     if (part == 0) {
-        int md = 2, X0 = 0, Y0 = 0;
+        int md = 2, X0 = 0, Y0 = 0, NX = 0, NY = 0;
         if (valid) {
             const float x0 = fx[g][0], y0 = fy[g][0];
             bool ok = fabsf(x0) < 1.0e7f && fabsf(y0) < 1.0e7f;  // false for NaN / inf / huge
@@ -82,10 +84,13 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
             md = ok ? 0 : 1;
             X0 = ok ? (int)x0 : 0;
             Y0 = ok ? (int)y0 : 0;
+            // corners span [x0, floor(ix_last) + 1]: monotone round trip, so the last sample bounds it
+            NX = ok ? (int)(fx[g][K - 1] - x0) + 2 : 0;
+            NY = ok ? (int)(fy[g][K - 1] - y0) + 2 : 0;
         }
-        mode[g] = md;
         org[g][0] = X0;
         org[g][1] = Y0;
+        org[g][2] = md | (NX << 8) | (NY << 16);
     }
     __syncthreads();
 
@@ -108,14 +113,16 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
         const bool live = it < ITEMS;
         const int gq = live ? it / S : 0;
         const int rx = it - gq * S;
-        const int x = org[gq][0] + rx, y0 = org[gq][1];
-        const bool colin = live && mode[gq] == 0 && (unsigned)x < (unsigned)w;
+        const int x = org[gq][0] + rx, y0 = org[gq][1], info = org[gq][2];
+        const int ny = (info >> 16) & 0xff;
+        // only the needed corner rectangle touches memory; the slack row/column reads 0 for free
+        const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) && (unsigned)x < (unsigned)w;
         const int base = (int)(gq * hw) + x;
         dst[c] = live ? gq * SP + rx : -1;
 #pragma unroll
         for (int ry = 0; ry < S; ++ry) {
             const int y = y0 + ry;
-            const int off = (colin && (unsigned)y < (unsigned)h) ? (base + y * w) * 4 : OOB;
+            const int off = (colin && ry < ny && (unsigned)y < (unsigned)h) ? (base + y * w) * 4 : OOB;
             vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
         }
     }
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
     __syncthreads();
 
     // ---- phase 2: outputs; lanes = queries -> coalesced channel-row stores
-    const int md = mode[g];
+    const int md = org[g][2] & 0xff;
     if (md == 2) return;
     float* __restrict__ outp = P.out + ((int64_t)b * P.C + (int64_t)lv * KK) * P.q_count + q0 + g;
     const int X0 = org[g][0], Y0 = org[g][1];

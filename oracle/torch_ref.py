@@ -31,7 +31,7 @@ class TorchCpuCorrBlock:
         B, _, H, W = coords.shape
         c = coords.permute(0, 2, 3, 1).reshape(B * H * W, 1, 1, 2)
         k = 2 * r + 1
-        steps = torch.linspace(-r, r, k)
+        steps = torch.linspace(-r, r, k).to(coords.device)   # corr.py:37-39 builds it on CPU, then .to()
         oy, ox = torch.meshgrid(steps, steps, indexing="ij")
         # last axis = (first meshgrid output, second) as in corr.py:39
         offs = torch.stack([oy, ox], dim=-1).view(1, k, k, 2)

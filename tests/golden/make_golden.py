@@ -178,6 +178,8 @@ def run_e2e(name, H, W, bins, subtype, seed, warm, up_stride):
 
 
 def main():
+    if "--e2e-only" in sys.argv:
+        return run_all_e2e()
     with open(os.path.join(HERE, "meta.json"), "w") as fh:
         json.dump(META, fh, indent=1)
     run_corr_case("t16x24", 1, 256, 16, 24, 4, 4, 10,
@@ -192,9 +194,14 @@ def main():
     run_large_case("mvsec32x32", 2, 32, 32, 2000)
     run_sampler()
     run_errors()
+    run_all_e2e()
+
+
+def run_all_e2e():
     run_e2e("small_standard", 128, 160, 15, "standard", 3000, False, 1)
     run_e2e("small_warm", 128, 160, 15, "warm_start", 3100, True, 1)
     run_e2e("dsec_standard", 480, 640, 15, "standard", 3200, False, 4)
+    run_e2e("mvsec_warm", 256, 256, 5, "warm_start", 3300, True, 1)
 
 
 if __name__ == "__main__":

@@ -1,14 +1,15 @@
 #!/bin/bash
+# Full GPU check: parity tests (incl. e2e and the 2-rank row-shard test), smoke, bench.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
-tail -5 gpurun_out/pytest_gpu.log
+grep -E 'PASSED|FAILED|ERROR|EPE|passed|failed' gpurun_out/pytest_gpu.log | tail -40
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
+rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log
 if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -2 gpurun_out/bench.log
 exit $rc
