@@ -7,7 +7,9 @@ Same constructor and call signatures as the reference:
     corr_fn.corr_pyramid[i] : [B*H*W, 1, h_i, w_i]                   # corr.py:16,24,27
 The work happens in libecorr.so (hand-written gfx950 HIP kernels, C ABI include/ecorr.h): one
 MFMA GEMM launch builds all 4 pyramid levels, one gather launch serves each lookup.  No ATen
-compute op runs on the hot path and there is no CPU fallback.
+compute op runs on the hot path and there is no CPU fallback.  The pyramid lives in a tiled,
+gather-friendly layout (layout.py); corr_pyramid materializes the reference-layout levels on
+first access (nothing on the E-RAFT path reads it).
 
 Contract differences, all loud: inputs must be fp32 HIP tensors (the reference path is fp32,
 eraft.py:104-105); the block is forward-only (E-RAFT only ever calls it under torch.no_grad(),
@@ -17,6 +19,7 @@ build's (B, 2, H, W) exactly.
 import torch
 
 from . import _lib
+from .layout import untile
 
 
 def _require_device_f32(name, t):
@@ -62,9 +65,17 @@ class CorrBlock:
             _lib.check(_lib.lib().ecorr_build(
                 fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, Q, num_levels,
                 self._pyramid.data_ptr(), _lib.stream_of(fmap1)), "CorrBlock build")
-        self.corr_pyramid = [
-            self._pyramid[self._off[i]:self._off[i + 1]].view(B * Q, 1, self._h[i], self._w[i])
-            for i in range(num_levels)]
+        self._rows = B * Q
+        self._levels_cache = None
+
+    @property
+    def corr_pyramid(self):
+        """Reference-layout levels [B*H*W, 1, h_i, w_i] (corr.py:16-27), materialized on demand."""
+        if self._levels_cache is None:
+            self._levels_cache = [
+                untile(self._pyramid[self._off[i]:self._off[i + 1]], self._rows, self._h[i], self._w[i])
+                for i in range(self.num_levels)]
+        return self._levels_cache
 
     def __call__(self, coords):
         B, _, H, W = self._shape
@@ -89,4 +100,4 @@ class CorrBlock:
         """Level-0 volume fmap1^T fmap2 / sqrt(D) as [B, H, W, 1, H, W] (corr.py:52-60)."""
         blk = CorrBlock(fmap1, fmap2, num_levels=1, radius=0)
         B, _, H, W = fmap1.shape
-        return blk._pyramid.view(B, H, W, 1, H, W)
+        return blk.corr_pyramid[0].view(B, H, W, 1, H, W)

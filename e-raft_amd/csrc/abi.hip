@@ -5,6 +5,7 @@
 // throws across the boundary.
 #include <math.h>
 
+#include "ecorr_device.h"
 #include "ecorr_internal.h"
 
 #define ECORR_EXPORT extern "C" __attribute__((visibility("default")))
@@ -24,7 +25,7 @@ int layout(int64_t rows, int H, int W, int levels, int* h, int* w, int64_t* off)
         if (h) h[i] = hh;
         if (w) w[i] = ww;
         if (off) off[i] = o;
-        o += rows * hh * ww;
+        o += rows * pad_h(hh) * pad_w(ww);   // tiled: each query image padded to 4 x 8 tiles
     }
     if (off) off[levels] = o;
     return ECORR_OK;
@@ -38,6 +39,13 @@ bool q_count_ok(int H, int W, int q_count) {
 }  // namespace
 
 ECORR_EXPORT int ecorr_abi_version(void) { return ECORR_ABI_VERSION; }
+
+ECORR_EXPORT int ecorr_pyramid_tile(int* tile_h, int* tile_w) {
+    if (!tile_h || !tile_w) return ECORR_EINVAL;
+    *tile_h = kTileH;
+    *tile_w = kTileW;
+    return ECORR_OK;
+}
 
 ECORR_EXPORT const char* ecorr_strerror(int status) {
     switch (status) {
@@ -93,7 +101,11 @@ ECORR_EXPORT int ecorr_lookup(const float* pyramid, const float* coords, int B, 
     int64_t off[ECORR_MAX_LEVELS + 1];
     const int st = layout((int64_t)B * q_count, H, W, levels, P.lh, P.lw, off);
     if (st != ECORR_OK) return st;
-    for (int i = 0; i < levels; ++i) P.lvl[i] = pyramid + off[i];
+    for (int i = 0; i < levels; ++i) {
+        P.lvl[i] = pyramid + off[i];
+        P.lntx[i] = pad_w(P.lw[i]) / kTileW;
+        P.lsz[i] = pad_h(P.lh[i]) * pad_w(P.lw[i]);
+    }
     P.coords = coords;
     P.out = out;
     P.H = H;

@@ -12,6 +12,15 @@ namespace ecorr {
 
 constexpr int kWave = 64;
 
+// Pyramid level storage (include/ecorr.h): each query's level image [h][w] is stored as
+// row-major 4 x 8-float tiles (128 B = one L2 line); ntx = padded width / 8 tiles per tile row.
+constexpr int kTileH = 4, kTileW = 8, kTile = kTileH * kTileW;
+__host__ __device__ __forceinline__ int tiled_off(int y, int x, int ntx) {
+    return (((y >> 2) * ntx + (x >> 3)) << 5) + ((y & 3) << 3) + (x & 7);
+}
+__host__ __device__ __forceinline__ int pad_h(int h) { return (h + kTileH - 1) & ~(kTileH - 1); }
+__host__ __device__ __forceinline__ int pad_w(int w) { return (w + kTileW - 1) & ~(kTileW - 1); }
+
 // model/utils.py:11-12 then ATen grid_sampler unnormalize (align_corners=True):
 //   g  = RN(RN(2x / (size-1)) - 1)
 //   ix = RN(RN(g + 1) * ((size-1)/2))
@@ -35,20 +44,25 @@ __device__ __forceinline__ float blend(float vnw, float vne, float vsw, float vs
 
 // Zeros-padding corner fetch by float coordinates (float compare: NaN and +-huge read 0, exactly
 // as ATen's int32-converted masks do).  Used by the generic / fallback paths only.
-__device__ __forceinline__ float corner(const float* __restrict__ img, int h, int w, float fx, float fy) {
+// ntx < 0: row-major image (bilinear_sampler); otherwise a tiled pyramid level.
+__device__ __forceinline__ float corner(const float* __restrict__ img, int h, int w, float fx, float fy,
+                                        int ntx = -1) {
     const bool in = (fx >= 0.0f) & (fx < (float)w) & (fy >= 0.0f) & (fy < (float)h);
-    return in ? img[(int64_t)(int)fy * w + (int)fx] : 0.0f;
+    if (!in) return 0.0f;
+    const int y = (int)fy, x = (int)fx;
+    return img[ntx < 0 ? (int64_t)y * w + x : (int64_t)tiled_off(y, x, ntx)];
 }
 
 // One bilinear sample of img[h][w] at pixel coordinates (x, y) (model/utils.py:7-21).
-__device__ __forceinline__ float sample_px(const float* __restrict__ img, int h, int w, float x, float y) {
+__device__ __forceinline__ float sample_px(const float* __restrict__ img, int h, int w, float x, float y,
+                                           int ntx = -1) {
     const float ix = unnormalize(x, (float)(w - 1), (float)(w - 1) * 0.5f);
     const float iy = unnormalize(y, (float)(h - 1), (float)(h - 1) * 0.5f);
     const float x0 = floorf(ix), y0 = floorf(iy);
     const float wx = __fsub_rn(ix, x0), wy = __fsub_rn(iy, y0);
     const float x1 = __fadd_rn(x0, 1.0f), y1 = __fadd_rn(y0, 1.0f);
-    return blend(corner(img, h, w, x0, y0), corner(img, h, w, x1, y0), corner(img, h, w, x0, y1),
-                 corner(img, h, w, x1, y1), wx, wy);
+    return blend(corner(img, h, w, x0, y0, ntx), corner(img, h, w, x1, y0, ntx),
+                 corner(img, h, w, x0, y1, ntx), corner(img, h, w, x1, y1, ntx), wx, wy);
 }
 
 }  // namespace ecorr

@@ -18,9 +18,9 @@ struct BuildParams {
     int n_mt, n_nt, n_ntx, n_tiles;
     int fused_levels;   // levels written by the GEMM epilogue (<= 4)
     int dev_skip_epilogue;  // A/B ablation only (ECORR_BUILD_SKIP_EPILOGUE): no pyramid stores
-    int dev_epilogue_v2;    // A/B only (ECORR_BUILD_OLD_EPILOGUE): per-thread scattered stores
     float* lvl[4];
-    int lh[4], lw[4];
+    int lntx[4], lnty[4];   // tiles per tile row / tile rows of each fused level
+    int64_t lsz[4];         // floats per query image of each fused level (padded to tiles)
 };
 
 int launch_build(const BuildParams& P, int B, int levels, const int* lh, const int* lw,
@@ -35,6 +35,8 @@ struct LookupParams {
     int C;                // levels * (2r+1)^2
     const float* lvl[ECORR_MAX_LEVELS];
     int lh[ECORR_MAX_LEVELS], lw[ECORR_MAX_LEVELS];
+    int lntx[ECORR_MAX_LEVELS];      // tiles per tile row
+    int lsz[ECORR_MAX_LEVELS];       // floats per query image (padded to tiles)
 };
 
 int launch_lookup(const LookupParams& P, int B, hipStream_t stream);

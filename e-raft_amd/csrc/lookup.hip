@@ -16,6 +16,8 @@
 //            256-byte coalesced row of the NCHW output.
 // Queries whose floors do not fit the staged window (NaN/inf/huge coordinates) take an exact
 // direct-gather path inside phase 2.
+#include <stdlib.h>
+
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
 
@@ -23,11 +25,13 @@ namespace ecorr {
 
 namespace {
 
-constexpr int QB = 64;   // queries per workgroup
-constexpr int NT = 256;
+constexpr int NT = 256;   // threads of the generic kernels
 
-template <int R>
-__global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
+// QB queries per workgroup, 4 threads per query (NTQ = 4 * QB threads); QB = 64 -> 4 waves,
+// QB = 16 -> one wave per workgroup (no cross-wave barrier; waves overlap phases freely).
+template <int R, int QB>
+__global__ __launch_bounds__(4 * QB) void lookup_staged(LookupParams P) {
+    constexpr int NTQ = 4 * QB;
     constexpr int K = 2 * R + 1;   // samples per axis
     constexpr int KK = K * K;
     constexpr int S = 2 * R + 3;   // staged window side
@@ -40,14 +44,14 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
     // Kept at 40 KB of LDS in total so 4 blocks fit a CU.
     __shared__ int org[QB][3];
 
-    const int tid = threadIdx.x, g = tid & (QB - 1), part = tid >> 6;
+    const int tid = threadIdx.x, g = tid & (QB - 1), part = tid / QB;
     const int lv = blockIdx.y, b = blockIdx.z;
-    const int h = P.lh[lv], w = P.lw[lv];
+    const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
     const int q0 = blockIdx.x * QB;                 // first query of the block (in the slab)
     const int p = q0 + g;
     const bool valid = p < P.q_count;
     const int64_t Q = P.q_count;                    // coords slab stride
-    const int64_t hw = (int64_t)h * w;
+    const int64_t hw = P.lsz[lv];                   // floats per query image (tiled, padded)
     const float* __restrict__ lvbase = P.lvl[lv] + ((int64_t)b * P.q_count + q0) * hw;
 
     // ---- phase 0: coordinate chains (corr.py:41-43, utils.py:11-12, grid_sampler unnormalize)
@@ -100,7 +104,7 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
     // offset and the hardware range check returns 0 -- zero padding with no branch and no select,
     // so all NCOL*S loads of a thread issue back to back.
     constexpr int ITEMS = QB * S;
-    constexpr int NCOL = (ITEMS + NT - 1) / NT;
+    constexpr int NCOL = (ITEMS + NTQ - 1) / NTQ;
     const int nq = min(QB, P.q_count - q0);
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lvbase), 0, (int)(nq * hw * 4), 0x00020000);
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
     int dst[NCOL];
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
-        const int it = tid + c * NT;
+        const int it = tid + c * NTQ;
         const bool live = it < ITEMS;
         const int gq = live ? it / S : 0;
         const int rx = it - gq * S;
@@ -117,12 +121,12 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
         const int ny = (info >> 16) & 0xff;
         // only the needed corner rectangle touches memory; the slack row/column reads 0 for free
         const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) && (unsigned)x < (unsigned)w;
-        const int base = (int)(gq * hw) + x;
+        const int base = (int)(gq * hw);
         dst[c] = live ? gq * SP + rx : -1;
 #pragma unroll
         for (int ry = 0; ry < S; ++ry) {
             const int y = y0 + ry;
-            const int off = (colin && ry < ny && (unsigned)y < (unsigned)h) ? (base + y * w) * 4 : OOB;
+            const int off = (colin && ry < ny && (unsigned)y < (unsigned)h) ? (base + tiled_off(y, x, ntx)) * 4 : OOB;
             vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
         }
     }
@@ -150,8 +154,8 @@ __global__ __launch_bounds__(NT) void lookup_staged(LookupParams P) {
             res = blend(c[0], c[1], c[S], c[S + 1], wa, nb);
         } else {
             const float xa1 = __fadd_rn(xa, 1.0f), yb1 = __fadd_rn(yb, 1.0f);
-            res = blend(corner(img, h, w, xa, yb), corner(img, h, w, xa1, yb),
-                        corner(img, h, w, xa, yb1), corner(img, h, w, xa1, yb1), wa, nb);
+            res = blend(corner(img, h, w, xa, yb, ntx), corner(img, h, w, xa1, yb, ntx),
+                        corner(img, h, w, xa, yb1, ntx), corner(img, h, w, xa1, yb1, ntx), wa, nb);
         }
         outp[(int64_t)k * P.q_count] = res;
     }
@@ -173,9 +177,9 @@ __global__ __launch_bounds__(NT) void lookup_direct(LookupParams P, int B) {
         const float inv = 1.0f / (float)(1 << lv);
         const float cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
         const float cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);
-        const float* img = P.lvl[lv] + ((int64_t)b * P.q_count + qq) * (int64_t)h * w;
+        const float* img = P.lvl[lv] + ((int64_t)b * P.q_count + qq) * (int64_t)P.lsz[lv];
         P.out[i] = sample_px(img, h, w, __fadd_rn(cx, (float)(a - P.radius)),
-                             __fadd_rn(cy, (float)(bb - P.radius)));
+                             __fadd_rn(cy, (float)(bb - P.radius)), P.lntx[lv]);
     }
 }
 
@@ -219,19 +223,30 @@ inline int hip_status() {
 
 }  // namespace
 
-int launch_lookup(const LookupParams& P, int B, hipStream_t stream) {
+template <int QB>
+static void launch_staged(const LookupParams& P, int B, hipStream_t stream) {
     const dim3 grid((unsigned)((P.q_count + QB - 1) / QB), (unsigned)P.levels, (unsigned)B);
+    const dim3 block(4 * QB);
     switch (P.radius) {
-        case 0: hipLaunchKernelGGL(lookup_staged<0>, grid, dim3(NT), 0, stream, P); break;
-        case 1: hipLaunchKernelGGL(lookup_staged<1>, grid, dim3(NT), 0, stream, P); break;
-        case 2: hipLaunchKernelGGL(lookup_staged<2>, grid, dim3(NT), 0, stream, P); break;
-        case 3: hipLaunchKernelGGL(lookup_staged<3>, grid, dim3(NT), 0, stream, P); break;
-        case 4: hipLaunchKernelGGL(lookup_staged<4>, grid, dim3(NT), 0, stream, P); break;
-        default: {
-            const int64_t n = (int64_t)B * P.C * P.q_count;
-            hipLaunchKernelGGL(lookup_direct, dim3(grid_for(n)), dim3(NT), 0, stream, P, B);
-        }
+        case 0: hipLaunchKernelGGL((lookup_staged<0, QB>), grid, block, 0, stream, P); break;
+        case 1: hipLaunchKernelGGL((lookup_staged<1, QB>), grid, block, 0, stream, P); break;
+        case 2: hipLaunchKernelGGL((lookup_staged<2, QB>), grid, block, 0, stream, P); break;
+        case 3: hipLaunchKernelGGL((lookup_staged<3, QB>), grid, block, 0, stream, P); break;
+        default: hipLaunchKernelGGL((lookup_staged<4, QB>), grid, block, 0, stream, P); break;
     }
+}
+
+int launch_lookup(const LookupParams& P, int B, hipStream_t stream) {
+    if (P.radius > 4) {
+        const int64_t n = (int64_t)B * P.C * P.q_count;
+        hipLaunchKernelGGL(lookup_direct, dim3(grid_for(n)), dim3(NT), 0, stream, P, B);
+        return hip_status();
+    }
+    // dev knob for A/B timing (tools/ab_lookup.py): ECORR_LOOKUP_QB = 16 | 64
+    const char* kq = getenv("ECORR_LOOKUP_QB");
+    const int qb = kq ? atoi(kq) : 64;
+    if (qb == 16) launch_staged<16>(P, B, stream);
+    else launch_staged<64>(P, B, stream);
     return hip_status();
 }
 

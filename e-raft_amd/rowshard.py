@@ -20,6 +20,7 @@ import torch.distributed as dist
 
 from . import _lib
 from .corr import _no_grad_inputs, _require_device_f32
+from .layout import untile
 
 
 def row_partition(H, world):
@@ -104,9 +105,17 @@ class RowShardedCorrBlock:
             _lib.check(_lib.lib().ecorr_build(
                 fmap1_rows.data_ptr(), fmap2.data_ptr(), B, D, H, W, self.q_count, num_levels,
                 self._pyramid.data_ptr(), _lib.stream_of(fmap2)), "RowShardedCorrBlock build")
-        self.corr_pyramid = [
-            self._pyramid[self._off[i]:self._off[i + 1]].view(B * self.q_count, 1, self._h[i], self._w[i])
-            for i in range(num_levels)]
+        self._levels_cache = None
+
+    @property
+    def corr_pyramid(self):
+        """This rank's levels in the reference layout [B*rows_r*W, 1, h_i, w_i] (a copy)."""
+        if self._levels_cache is None:
+            rows = self._shape[0] * self.q_count
+            self._levels_cache = [
+                untile(self._pyramid[self._off[i]:self._off[i + 1]], rows, self._h[i], self._w[i])
+                for i in range(self.num_levels)]
+        return self._levels_cache
 
     def lookup_local(self, coords_rows):
         """Lookup for this rank's query rows: coords [B, 2, rows_r, W] -> [B, C, rows_r, W]."""

@@ -5,6 +5,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -50,7 +51,12 @@ def test_layout_matches_reference_shapes(ea):
     from eraft_amd import _lib
     h, w, off = _lib.layout(16 * 4800, 60, 80, 4)
     assert (h, w) == ([60, 30, 15, 7], [80, 40, 20, 10])
-    assert off == [0, 368640000, 460800000, 483840000, 489216000]
+    # tiled storage: each image padded to 4 x 8 tiles (60x80, 32x40, 16x24, 8x16)
+    sizes = [60 * 80, 32 * 40, 16 * 24, 8 * 16]
+    assert off == [0] + list(np.cumsum([76800 * s for s in sizes]))
+    th, tw = ctypes.c_int(), ctypes.c_int()
+    assert ea.lib().ecorr_pyramid_tile(ctypes.byref(th), ctypes.byref(tw)) == 0
+    assert (th.value, tw.value) == (4, 8)
     h, w, _ = _lib.layout(396, 18, 22, 4)
     assert (h, w) == ([18, 9, 4, 2], [22, 11, 5, 2])
 
@@ -80,3 +86,17 @@ def test_cpu_tensors_rejected_loudly(ea):
     f = torch.zeros(1, 16, 8, 8)
     with pytest.raises(RuntimeError, match="HIP"):
         ea.CorrBlock(f, f)
+
+
+def test_tile_untile_roundtrip():
+    import torch
+    from eraft_amd.layout import tile, untile
+    for (h, w) in [(60, 80), (15, 20), (7, 10), (1, 1), (9, 11)]:
+        lv = torch.arange(3 * h * w, dtype=torch.float32).reshape(3, h, w)
+        flat = tile(lv)
+        hp, wp = -(-h // 4) * 4, -(-w // 8) * 8
+        assert flat.numel() == 3 * hp * wp
+        assert torch.equal(untile(flat, 3, h, w)[:, 0], lv)
+        # element (y, x) of image r lives at r*hp*wp + ((y//4)*(wp//8) + x//8)*32 + (y%4)*8 + x%8
+        r, y, x = 2, h - 1, w - 1
+        assert flat[r * hp * wp + ((y // 4) * (wp // 8) + x // 8) * 32 + (y % 4) * 8 + x % 8] == lv[r, y, x]

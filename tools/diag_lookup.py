@@ -17,7 +17,8 @@ case = sys.argv[1] if len(sys.argv) > 1 else "b2_8x12"
 z = np.load(os.path.join(ROOT, "tests", "golden", f"corr_{case}.npz"))
 L, r = int(z["L"]), int(z["r"])
 levels = [z[f"level{i}"] for i in range(L)]
-flat = torch.from_numpy(np.concatenate([lv.reshape(-1) for lv in levels])).cuda()
+from eraft_amd.layout import tile  # noqa: E402
+flat = torch.cat([tile(torch.from_numpy(lv)) for lv in levels]).cuda()
 K = 2 * r + 1
 for k in z.files:
     if not k.startswith("coords_"):
