@@ -3,17 +3,23 @@
 
 One step = one pass of the hot path over one batch: CorrBlock build (fp32-MFMA GEMM + fused
 pyramid) followed by the 12 GRU-iteration lookups, exactly the call pattern of ERAFT.forward
-(eraft.py:107, 126-128), with inputs already resident in HBM.  Workload at N=1 = BASELINE
-configs[1]: DSEC 480x640 (fmaps 256 x 60 x 80), batch 16, warm-start coordinates (12 distinct
-coordinate fields = coords_grid + smooth flow + per-iteration jitter).  N>1 (configs[3]): one
-process per GPU, each with its own batch of pairs, no data-path collective ("weak" scaling).
+(eraft.py:107, 126-128), with inputs already resident in HBM.
+
+  default (--mode batch): BASELINE configs[1] at N=1 -- DSEC 480x640 (fmaps 256 x 60 x 80), batch
+      16 per GPU, warm-start coordinates (12 distinct coordinate fields = coords_grid + smooth
+      flow + per-iteration jitter).  N>1 = configs[3]: one process per GPU, each with its own
+      batch of pairs, no data-path collective ("weak" scaling).
+  --mode rowshard: BASELINE configs[4] -- 1280x720 (fmap 256 x 92 x 160, padded 736 rows), batch
+      4, query rows sharded over the N ranks, fmap2 row slabs all-gathered once per pair and the
+      lookup output slabs once per iteration over RCCL ("strong" scaling).
 
     python bench.py [--gpus N --steps K --warmup W --batch 16 --no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 
 Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP-event timed over the timed
-region) and `cpu_baseline` (the torch-CPU restatement of the reference, oracle/torch_ref.py, timed
-on this host's cores on a bounded sample).
+region on the launch stream) and `cpu_baseline` (the torch-CPU restatement of the reference,
+oracle/torch_ref.py, timed on this host's cores on a bounded sample, rank 0 at N=1 only).
+BENCH_SINGLE_DEVICE=1 puts every rank on cuda:0 with gloo (multi-process rehearsal on one GPU).
 """
 import argparse
 import json
@@ -37,21 +43,29 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=16, help="frame pairs per GPU")
-    ap.add_argument("--height", type=int, default=60, help="fmap rows (480/8)")
-    ap.add_argument("--width", type=int, default=80, help="fmap cols (640/8)")
+    ap.add_argument("--mode", choices=("batch", "rowshard"), default="batch")
+    ap.add_argument("--batch", type=int, default=None, help="pairs per GPU (batch) / per job (rowshard)")
+    ap.add_argument("--height", type=int, default=None, help="fmap rows")
+    ap.add_argument("--width", type=int, default=None, help="fmap cols")
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.mode == "batch":
+        a.batch, a.height, a.width = a.batch or 16, a.height or 60, a.width or 80
+    else:
+        a.batch, a.height, a.width = a.batch or 4, a.height or 92, a.width or 160
+    return a
 
 
-def algorithmic(B, D, H, W, L=4, r=4):
-    """build flops 2*B*Q^2*D; lookup bytes B*Q*[L(2r+2)^2*4 + L(2r+1)^2*4 + 8]."""
+def algorithmic(B, D, H, W, L=4, r=4, q=None):
+    """build flops 2*B*q*Q*D; lookup bytes B*q*[L(2r+2)^2*4 + L(2r+1)^2*4 + 8]
+    (q = query pixels served, Q = H*W targets)."""
     Q = H * W
-    flops = 2.0 * B * Q * Q * D
-    look_bytes = B * Q * (L * (2 * r + 2) ** 2 * 4 + L * (2 * r + 1) ** 2 * 4 + 2 * 4)
+    q = Q if q is None else q
+    flops = 2.0 * B * q * Q * D
+    look_bytes = B * q * (L * (2 * r + 2) ** 2 * 4 + L * (2 * r + 1) ** 2 * 4 + 2 * 4)
     return flops, look_bytes
 
 
@@ -99,8 +113,22 @@ def cpu_baseline(B, D, H, W, iters, seconds):
         if el >= seconds or pairs >= 64:
             break
     return {"value": pairs / el, "unit": "pairs/s", "cores": cores, "kind": "port",
-            "sample": f"{pairs} DSEC pairs ({nb} per step, fmap {D}x{H}x{W}, build + {iters} lookups) "
-                      f"in {el:.1f} s; torch {torch.__version__} CPU ops = reference's ATen ops"}
+            "sample": f"{pairs} pairs ({nb} per step, fmap {D}x{H}x{W}, build + {iters} lookups) in "
+                      f"{el:.1f} s; torch {torch.__version__} CPU ops = the reference's ATen ops"}
+
+
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per dispatch of the dominant kernel from the committed PMC summary of this same
+    bench command (profiles/latest_pmc.json, written by tools/pmc_summary.py), else None."""
+    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
+    try:
+        js = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    for name, rec in js.get("kernels", {}).items():
+        if name.startswith(kernel_prefix) and "hbm_bytes" in rec:
+            return rec["hbm_bytes"], f"{js.get('source', path)}: {name} ({rec.get('read_correction')})"
+    return None, None
 
 
 def main():
@@ -108,21 +136,45 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+    single = os.environ.get("BENCH_SINGLE_DEVICE") == "1"
+    dev_index = 0 if single else local
+    device = torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
+    distributed = world > 1 or a.mode == "rowshard"
+    if distributed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")   # plain `python bench.py --mode rowshard`
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        backend = "gloo" if single else "nccl"
+        kw = {} if single else {"device_id": device}
+        dist.init_process_group(backend, **kw)
     import eraft_amd
 
     B, D, H, W, iters = a.batch, a.dim, a.height, a.width, a.iters
-    f1, f2, coords = make_inputs(B, D, H, W, iters, device, seed=1234 + rank)
     stream = torch.cuda.current_stream(device)
+    if a.mode == "batch":
+        f1, f2, coords = make_inputs(B, D, H, W, iters, device, seed=1234 + rank)
+
+        def make_block():
+            return eraft_amd.CorrBlock(f1, f2, num_levels=4, radius=4)
+        q_local = H * W
+    else:
+        from eraft_amd.rowshard import RowShardedCorrBlock, row_partition
+        f1, f2, coords = make_inputs(B, D, H, W, iters, device, seed=1234)   # same job on every rank
+        starts, counts = row_partition(H, world)
+        r0, rr = starts[rank], counts[rank]
+        f1_rows = f1[:, :, r0:r0 + rr].contiguous()
+        f2_rows = f2[:, :, r0:r0 + rr].contiguous()
+
+        def make_block():
+            return RowShardedCorrBlock.from_row_slabs(f1_rows, f2_rows, H)
+        q_local = rr * W
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        blk = eraft_amd.CorrBlock(f1, f2, num_levels=4, radius=4)
+        blk = make_block()
         if ev is not None:
             ev[1].record(stream)
         for c in coords:
@@ -135,7 +187,7 @@ def main():
         for _ in range(a.warmup):
             step()
         torch.cuda.synchronize()
-        if world > 1:
+        if distributed:
             dist.barrier()
         torch.cuda.synchronize()
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
@@ -143,53 +195,64 @@ def main():
         for k in range(a.steps):
             step(evs[k])
         torch.cuda.synchronize()
-        if world > 1:
+        if distributed:
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
 
     build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps
     look_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps / iters
-    if world > 1:
-        t = torch.tensor([elapsed, build_ms, look_ms], device=device, dtype=torch.float64)
+    if distributed:
+        t = torch.tensor([elapsed, build_ms, look_ms], dtype=torch.float64,
+                         device="cpu" if single else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, build_ms, look_ms = t.tolist()
 
-    flops, look_bytes = algorithmic(B, D, H, W)
+    flops, look_bytes = algorithmic(B, D, H, W, q=q_local)
     build_tf = flops / (build_ms * 1e-3) / 1e12
     look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
+    note = "" if a.mode == "batch" else " (per rank; lookup time includes the output all-gather)"
     kernels = {
         "build": {"bound": "mfma", "achieved": round(build_tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
                   "unit": "TFLOP/s", "frac": round(build_tf / PEAK_FP32_MFMA_TFLOPS, 4),
-                  "ms_per_launch": round(build_ms, 4), "work_per_launch": f"{flops:.4g} flop"},
+                  "ms_per_launch": round(build_ms, 4), "work_per_launch": f"{flops:.4g} flop" + note},
         "lookup": {"bound": "hbm", "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                    "frac": round(look_gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(look_ms, 4),
-                   "launches_per_step": iters, "work_per_launch": f"{look_bytes:.4g} B"},
+                   "launches_per_step": iters, "work_per_launch": f"{look_bytes:.4g} B" + note},
     }
     dom = "build" if build_ms >= look_ms * iters else "lookup"
     roof = {k: kernels[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")}
     roof["kernel"] = dom
-    roof["traffic"] = None
+    traffic, src = pmc_traffic("build_kernel" if dom == "build" else "lookup_staged")
+    roof["traffic"] = traffic
+    if src:
+        roof["traffic_source"] = src
     ideal_s = flops / (PEAK_FP32_MFMA_TFLOPS * 1e12) + iters * look_bytes / (PEAK_HBM_GBS * 1e9)
-    pairs = world * B * a.steps
+    pairs = (world * B if a.mode == "batch" else B) * a.steps
+    if a.mode == "batch":
+        cfg = {"workload": f"DSEC 480x640 CorrBlock build + {iters} lookups, warm-start, batch {B} per GPU "
+                           f"(BASELINE configs[1]; N>1 = configs[3])",
+               "global_batch": world * B, "fmap": [D, H, W], "levels": 4, "radius": 4,
+               "parallelism": f"dp{world} batch-sharded, no collective"}
+    else:
+        cfg = {"workload": f"1280x720 CorrBlock build + {iters} lookups, batch {B}, query rows sharded "
+                           f"over {world} GPUs (BASELINE configs[4])",
+               "global_batch": B, "fmap": [D, H, W], "levels": 4, "radius": 4,
+               "parallelism": f"query-row shard x{world}, RCCL all-gather of fmap2 + output slabs"}
     res = {
         "metric": METRIC, "value": round(pairs / elapsed, 2), "unit": "pairs/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak" if a.mode == "batch" else "strong",
+        "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (randn fmaps, coords_grid + smooth warm-start flow)",
-        "config": {"workload": f"DSEC 480x640 CorrBlock build + {iters} lookups, warm-start, "
-                               f"batch {B} per GPU (BASELINE configs[1]; N>1 = configs[3])",
-                   "global_batch": world * B, "fmap": [D, H, W], "levels": 4, "radius": 4,
-                   "parallelism": f"dp{world} batch-sharded, no collective"},
-        "roofline": roof,
-        "kernels": kernels,
+        "config": cfg, "roofline": roof, "kernels": kernels,
         "corrblock_frac": round(ideal_s / (elapsed / a.steps), 4),
     }
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(B, D, H, W, iters, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

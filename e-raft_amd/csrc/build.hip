@@ -32,13 +32,14 @@ namespace {
 constexpr int BM = 128;           // queries per block tile
 constexpr int TBH = 8, TBW = 16;  // target block (rows x cols) per block tile
 constexpr int BN = TBH * TBW;     // 128 targets
-constexpr int BK = 32;            // K chunk
 constexpr int NT = 256;           // threads
 constexpr int CS = BN + 4;        // C-tile LDS row stride (floats): conflict-free ds_read_b128
-constexpr int STAGE_FLOATS = 2 * (BK * BM + BK * BN);
-constexpr int CTILE_FLOATS = BM * CS;
-constexpr int SMEM_FLOATS = STAGE_FLOATS > CTILE_FLOATS ? STAGE_FLOATS : CTILE_FLOATS;
 constexpr int P1S = 36, P2S = 12;  // LDS per-query strides of the pooled staging (conflict-free)
+
+// LDS floats for K chunk KB (double-buffered A and B) and a C tile of MR query rows.
+constexpr int smem_floats(int KB, int MR) {
+    return 2 * (KB * BM + KB * BN) > MR * CS ? 2 * (KB * BM + KB * BN) : MR * CS;
+}
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -76,20 +77,22 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
 }
 
-// Epilogue (all threads; contains barriers).  Cs = scaled 128 x 128 C tile ([m][n], stride CS,
-// n = ty*16 + tx).  Level 0: 4 whole tiles per query (two 256-byte pieces), 32 float4 per query.
+// Epilogue (all threads; contains barriers).  Cs = scaled C-tile rows ([m][n], stride CS,
+// n = ty*16 + tx) of MR of the block's queries (all 128, or one half of them).  Level 0: 4 whole tiles per query (two 256-byte pieces), 32 float4 per query.
 // Pooling: thread (query m, 8x8 block blk) reduces in registers 8x8 -> 4x4 -> 2x2 -> 1, each level
 // from the rounded previous one, parks levels 1-3 in LDS, then level 1 leaves as one whole tile
 // per query, level 2 as two 16-byte rows, level 3 as 8 bytes.  Tiles beyond a level's padded
 // extent are skipped; padding cells inside a tile are written but never read.
-__device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& tc, float* Cs, int tid) {
-    const int64_t row0 = (int64_t)tc.b * P.q_count + tc.m0;
-    const int mvalid = min(BM, P.q_count - tc.m0);
+template <int MR>
+__device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& tc, float* Cs, int tid, int mlo) {
+    // Cs holds C-tile rows [mlo, mlo + MR) of the block's 128 queries
+    const int64_t row0 = (int64_t)tc.b * P.q_count + tc.m0 + mlo;
+    const int mvalid = min(MR, P.q_count - tc.m0 - mlo);
     {   // level 0
         const int ntx = P.lntx[0], nty = P.lnty[0];
         const int tr0 = tc.ty0 / kTileH, tc0 = tc.tx0 / kTileW;
 #pragma unroll 4
-        for (int s = 0; s < (BM * 32) / NT; ++s) {
+        for (int s = 0; s < (MR * 32) / NT; ++s) {
             const int idx = tid + NT * s;
             const int m = idx >> 5, rem = idx & 31;
             const int trl = rem >> 4, tcl = (rem >> 3) & 1, j = rem & 7;
@@ -102,9 +105,10 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
         }
     }
     if (P.fused_levels < 2) return;   // uniform over the block
-    const int m = tid & (BM - 1), blk = tid >> 7;
-    float l1[4][4], l2[2][2], l3;
-    {
+    const bool pooler = tid < 2 * MR;
+    const int m = tid % MR, blk = tid / MR;
+    float l1[4][4], l2[2][2], l3 = 0.0f;
+    if (pooler) {
         float v[8][8];
 #pragma unroll
         for (int ty = 0; ty < 8; ++ty) {
@@ -118,31 +122,33 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
 #pragma unroll
             for (int x = 0; x < 4; ++x)
                 l1[y][x] = pool4(v[2 * y][2 * x], v[2 * y][2 * x + 1], v[2 * y + 1][2 * x], v[2 * y + 1][2 * x + 1]);
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+                l2[y][x] = pool4(l1[2 * y][2 * x], l1[2 * y][2 * x + 1], l1[2 * y + 1][2 * x], l1[2 * y + 1][2 * x + 1]);
+        l3 = pool4(l2[0][0], l2[0][1], l2[1][0], l2[1][1]);
     }
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-            l2[y][x] = pool4(l1[2 * y][2 * x], l1[2 * y][2 * x + 1], l1[2 * y + 1][2 * x], l1[2 * y + 1][2 * x + 1]);
-    l3 = pool4(l2[0][0], l2[0][1], l2[1][0], l2[1][1]);
     __syncthreads();   // all reads of Cs done: reuse it for the pooled staging
-    float* S1 = Cs;                       // [BM][4 rows][8 cols] = the level-1 tile, stride P1S
-    float* S2 = Cs + BM * P1S;            // [BM][2 rows][4 cols], stride P2S
-    float* S3 = S2 + BM * P2S;            // [BM][2 cols]
+    float* S1 = Cs;                       // [MR][4 rows][8 cols] = the level-1 tile, stride P1S
+    float* S2 = Cs + MR * P1S;            // [MR][2 rows][4 cols], stride P2S
+    float* S3 = S2 + MR * P2S;            // [MR][2 cols]
+    if (pooler) {
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
-        *reinterpret_cast<floatx4*>(S1 + m * P1S + y * 8 + blk * 4) = floatx4{l1[y][0], l1[y][1], l1[y][2], l1[y][3]};
+        for (int y = 0; y < 4; ++y)
+            *reinterpret_cast<floatx4*>(S1 + m * P1S + y * 8 + blk * 4) = floatx4{l1[y][0], l1[y][1], l1[y][2], l1[y][3]};
 #pragma unroll
-    for (int y = 0; y < 2; ++y)
-        *reinterpret_cast<floatx2*>(S2 + m * P2S + y * 4 + blk * 2) = floatx2{l2[y][0], l2[y][1]};
-    S3[m * 2 + blk] = l3;
+        for (int y = 0; y < 2; ++y)
+            *reinterpret_cast<floatx2*>(S2 + m * P2S + y * 4 + blk * 2) = floatx2{l2[y][0], l2[y][1]};
+        S3[m * 2 + blk] = l3;
+    }
     __syncthreads();
     {   // level 1: tile (ty0/8, tx0/16), 8 float4 per query
         const int tr = tc.ty0 / 8, tcc = tc.tx0 / 16;
         if (tr < P.lnty[1] && tcc < P.lntx[1]) {
             float* base = P.lvl[1] + (tr * P.lntx[1] + tcc) * kTile;
 #pragma unroll
-            for (int s = 0; s < (BM * 8) / NT; ++s) {
+            for (int s = 0; s < (MR * 8) / NT; ++s) {
                 const int idx = tid + NT * s;
                 const int mm = idx >> 3, j = idx & 7;
                 if (mm < mvalid)
@@ -151,7 +157,7 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
             }
         }
     }
-    if (P.fused_levels >= 3) {   // level 2: rows (ty0/4)&3 + {0,1}, cols (tx0/4)&7 .. +3
+    if (P.fused_levels >= 3 && tid < 2 * MR) {   // level 2: rows (ty0/4)&3 + {0,1}, cols (tx0/4)&7 .. +3
         const int tr = tc.ty0 / 16, tcc = tc.tx0 / 32;
         const int mm = tid >> 1, y = tid & 1;
         if (tr < P.lnty[2] && tcc < P.lntx[2] && mm < mvalid) {
@@ -160,7 +166,7 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
                 *reinterpret_cast<const floatx4*>(S2 + mm * P2S + y * 4);
         }
     }
-    if (P.fused_levels >= 4 && tid < BM) {   // level 3: row (ty0/8)&3, cols (tx0/8)&7 .. +1
+    if (P.fused_levels >= 4 && tid < MR) {   // level 3: row (ty0/8)&3, cols (tx0/8)&7 .. +1
         const int tr = tc.ty0 / 32, tcc = tc.tx0 / 64;
         if (tr < P.lnty[3] && tcc < P.lntx[3] && tid < mvalid) {
             const int r = (tc.ty0 / 8) & 3, c0 = (tc.tx0 / 8) & 7;
@@ -170,11 +176,15 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
     }
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(NT, 2) void build_kernel(BuildParams P) {
-    __shared__ __attribute__((aligned(16))) float smem[SMEM_FLOATS];
-    float* As = smem;                       // [2][BK][BM]
-    float* Bs = smem + 2 * BK * BM;         // [2][BK][BN]
+// KB = K chunk depth; HALF = C tile handled in two 64-query halves.  KB = 16 + HALF needs 34 KB of
+// LDS and <= 168 VGPRs, so 3 blocks (3 waves per SIMD) share a CU; KB = 32 uses 67.5 KB (2 blocks).
+template <bool VEC, int KB, bool HALF>
+__global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) {
+    constexpr int MR = HALF ? BM / 2 : BM;
+    constexpr int NLD = (KB * BM / 4) / NT;   // float4 of A (and of B) per thread per chunk
+    __shared__ __attribute__((aligned(16))) float smem[smem_floats(KB, MR)];
+    float* As = smem;                       // [2][KB][BM]
+    float* Bs = smem + 2 * KB * BM;         // [2][KB][BN]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TileCoord tc = decode_tile(P, xcd_remap(blockIdx.x, gridDim.x));
@@ -185,11 +195,11 @@ __global__ __launch_bounds__(NT, 2) void build_kernel(BuildParams P) {
     const float* __restrict__ A = P.f1 + (int64_t)tc.b * D * QA;
     const float* __restrict__ Bm = P.f2 + (int64_t)tc.b * D * Q;
 
-    // ---- global -> register staging: 4 float4 of A and 4 of B per thread per K chunk ----
-    floatx4 ra[4], rb[4];
+    // ---- global -> register staging: NLD float4 of A and of B per thread per K chunk ----
+    floatx4 ra[NLD], rb[NLD];
     auto load_chunk = [&](int k0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NLD; ++i) {
             const int s = tid + NT * i;
             const int k = k0 + (s >> 5);
             {   // A: row k, queries m0 + 4c .. +3
@@ -221,11 +231,11 @@ __global__ __launch_bounds__(NT, 2) void build_kernel(BuildParams P) {
     };
     auto store_chunk = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NLD; ++i) {
             const int s = tid + NT * i;
             const int kk = s >> 5, c = s & 31;
-            *reinterpret_cast<floatx4*>(As + (buf * BK + kk) * BM + 4 * c) = ra[i];
-            *reinterpret_cast<floatx4*>(Bs + (buf * BK + kk) * BN + 4 * c) = rb[i];
+            *reinterpret_cast<floatx4*>(As + (buf * KB + kk) * BM + 4 * c) = ra[i];
+            *reinterpret_cast<floatx4*>(Bs + (buf * KB + kk) * BN + 4 * c) = rb[i];
         }
     };
 
@@ -240,18 +250,18 @@ __global__ __launch_bounds__(NT, 2) void build_kernel(BuildParams P) {
     // MFMA 32x32x2 f32 operand maps: lane l holds A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31]
     const int wm = wave & 1, wn = wave >> 1;
     const int arow = lane >> 5, acol = lane & 31;
-    const int nk = (D + BK - 1) / BK;
+    const int nk = (D + KB - 1) / KB;
 
     load_chunk(0);
     store_chunk(0);
     __syncthreads();
     for (int kc = 0; kc < nk; ++kc) {
         const int buf = kc & 1;
-        if (kc + 1 < nk) load_chunk((kc + 1) * BK);
-        const float* as = As + buf * BK * BM + wm * 64 + acol;
-        const float* bs = Bs + buf * BK * BN + wn * 64 + acol;
+        if (kc + 1 < nk) load_chunk((kc + 1) * KB);
+        const float* as = As + buf * KB * BM + wm * 64 + acol;
+        const float* bs = Bs + buf * KB * BN + wn * 64 + acol;
 #pragma unroll
-        for (int kk = 0; kk < BK; kk += 2) {
+        for (int kk = 0; kk < KB; kk += 2) {
             const int ro = kk + arow;
             const float a0 = as[ro * BM], a1 = as[ro * BM + 32];
             const float b0 = bs[ro * BN], b1 = bs[ro * BN + 32];
@@ -268,19 +278,25 @@ __global__ __launch_bounds__(NT, 2) void build_kernel(BuildParams P) {
     //      row = (reg&3) + 8*(reg>>2) + 4*(lane>>5) ----
     float* Cs = smem;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int half = 0; half < (HALF ? 2 : 1); ++half) {
+        if (!HALF || wm == half) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
-                const int n = wn * 64 + j * 32 + acol;
-                const float v = acc[i][j][r];
-                Cs[m * CS + n] = P.scale_is_mul ? __fmul_rn(v, P.scale) : __fdiv_rn(v, P.scale);
-            }
-    __syncthreads();
-    if (P.dev_skip_epilogue) return;
-    epilogue(P, tc, Cs, tid);
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = (HALF ? 0 : wm * 64) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
+                        const int n = wn * 64 + j * 32 + acol;
+                        const float v = acc[i][j][r];
+                        Cs[m * CS + n] = P.scale_is_mul ? __fmul_rn(v, P.scale) : __fdiv_rn(v, P.scale);
+                    }
+        }
+        __syncthreads();
+        if (P.dev_skip_epilogue) continue;
+        epilogue<MR>(P, tc, Cs, tid, half * MR);
+        if (HALF && half == 0) __syncthreads();   // half 0 fully consumed before half 1 overwrites Cs
+    }
 }
 
 // Levels beyond the 3 fused ones (num_levels > 4): plain 2x2 floor-mode pooling, tiled in and
@@ -326,10 +342,14 @@ int launch_build(const BuildParams& P0, int B, int levels, const int* lh, const 
     const bool vec = (P.W % 4 == 0) && (P.q_count % 4 == 0) && ((uintptr_t)P.f1 % 16 == 0) &&
                      ((uintptr_t)P.f2 % 16 == 0);
     if ((uintptr_t)lvl[0] % 16 != 0) return ECORR_EINVAL;   // tile stores are 16-byte vectors
-    if (vec)
-        hipLaunchKernelGGL(build_kernel<true>, dim3((unsigned)ntiles), dim3(NT), 0, stream, P);
-    else
-        hipLaunchKernelGGL(build_kernel<false>, dim3((unsigned)ntiles), dim3(NT), 0, stream, P);
+    // dev knob for A/B (tools/ab_build.py): ECORR_BUILD_KB32=1 selects the K=32, full-C-tile,
+    // 2-blocks-per-CU variant
+    const char* kv = getenv("ECORR_BUILD_KB32");
+    const bool kb32 = kv && atoi(kv) == 1;
+    const dim3 grid((unsigned)ntiles), block(NT);
+    if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true>), grid, block, 0, stream, P);
+    else if (kb32) hipLaunchKernelGGL((build_kernel<true, 32, false>), grid, block, 0, stream, P);
+    else hipLaunchKernelGGL((build_kernel<true, 16, true>), grid, block, 0, stream, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ECORR_EHIP - (int)e;
     const int64_t rows = (int64_t)B * P.q_count;

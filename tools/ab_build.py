@@ -12,10 +12,11 @@ sys.path.insert(0, ROOT)
 import eraft_amd  # noqa: E402
 
 VARIANTS = {
-    "build": {},
-    "build_noepi": {"ECORR_BUILD_SKIP_EPILOGUE": "1"},
+    "kb16_half": {},
+    "kb32_full": {"ECORR_BUILD_KB32": "1"},
+    "kb16_noepi": {"ECORR_BUILD_SKIP_EPILOGUE": "1"},
 }
-KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE",)
+KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32")
 B = int(os.environ.get("AB_BATCH", "16"))
 H, W, D = 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)

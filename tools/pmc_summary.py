@@ -1,13 +1,26 @@
 #!/usr/bin/env python3
 """Summarize rocprofv3 --pmc CSVs (one dir per pass) into per-kernel averages per dispatch.
-usage: tools/pmc_summary.py gpurun_out/<tag> > profiles/<tag>/pmc_summary.txt"""
+
+usage: tools/pmc_summary.py gpurun_out/<tag> [profiles/<tag>]
+Writes <out>/pmc_summary.txt (human) and <out>/pmc_summary.json (bench.py reads the HBM traffic
+of its dominant kernel from profiles/latest_pmc.json, a copy of the newest summary).
+
+HBM traffic per dispatch, corrected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
+coalesced read, so read bytes = 2 * FETCH_SIZE * 1024 for kernels whose loads are 16-byte
+vectors (the build).  The lookup's dword buffer loads are an uncalibrated width: its read bytes
+are reported uncorrected (1 * FETCH_SIZE) and flagged.  Infinity-Cache hits count as fabric
+traffic (the counters sit at the L2's memory side).
+"""
 import collections
 import csv
 import glob
+import json
 import os
 import sys
 
 root = sys.argv[1]
+out = sys.argv[2] if len(sys.argv) > 2 else None
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "pmc*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
@@ -15,11 +28,30 @@ for f in sorted(glob.glob(os.path.join(root, "pmc*", "*counter_collection.csv"))
         if "ecorr" not in name:
             continue
         name = name.replace("void ", "").replace("ecorr::(anonymous namespace)::", "")
-        name = name.split("(ecorr")[0].split("(int")[0]
+        name = name.split("(ecorr")[0].split("(int")[0].split("(float")[0]
         agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-print("# per-dispatch averages (FETCH_SIZE / WRITE_SIZE in KB as reported; gfx950 FETCH_SIZE reads")
-print("# ~1/2 of wide streaming bytes, MI355X_MICROARCH.md §HBM)")
+lines = ["# per-dispatch averages (FETCH_SIZE / WRITE_SIZE in KiB as reported; gfx950 FETCH_SIZE reads",
+         "# ~1/2 of wide streaming bytes, MI355X_MICROARCH.md §HBM)"]
+js = {}
 for k, d in sorted(agg.items()):
-    print(k)
-    for c, v in sorted(d.items()):
-        print(f"  {c:28s} {sum(v) / len(v):16.1f}   (n={len(v)})")
+    lines.append(k)
+    avg = {c: sum(v) / len(v) for c, v in d.items()}
+    for c, v in sorted(avg.items()):
+        lines.append(f"  {c:28s} {v:16.1f}   (n={len(d[c])})")
+    wide = k.startswith("build_kernel")
+    rec = {"counters": avg}
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        rd = avg["FETCH_SIZE"] * 1024 * (2 if wide else 1)
+        wr = avg["WRITE_SIZE"] * 1024
+        rec.update(read_bytes=rd, write_bytes=wr, hbm_bytes=rd + wr,
+                   read_correction="x2 (16-B/lane loads)" if wide else "none (dword loads, uncalibrated)")
+        lines.append(f"  => HBM bytes/dispatch {rd + wr:.4g} (read {rd:.4g} {rec['read_correction']}, write {wr:.4g})")
+    if "GRBM_GUI_ACTIVE" in avg:
+        rec["grbm_gui_active"] = avg["GRBM_GUI_ACTIVE"]
+    js[k] = rec
+txt = "\n".join(lines)
+print(txt)
+if out:
+    os.makedirs(out, exist_ok=True)
+    open(os.path.join(out, "pmc_summary.txt"), "w").write(txt + "\n")
+    json.dump({"source": root, "kernels": js}, open(os.path.join(out, "pmc_summary.json"), "w"), indent=1)
