@@ -19,7 +19,7 @@ build's (B, 2, H, W) exactly.
 import torch
 
 from . import _lib
-from .layout import untile
+from .layout import formats, untile
 
 
 def _require_device_f32(name, t):
@@ -72,8 +72,10 @@ class CorrBlock:
     def corr_pyramid(self):
         """Reference-layout levels [B*H*W, 1, h_i, w_i] (corr.py:16-27), materialized on demand."""
         if self._levels_cache is None:
+            ntx = formats(self._shape[2], self._shape[3], self.num_levels)
             self._levels_cache = [
-                untile(self._pyramid[self._off[i]:self._off[i + 1]], self._rows, self._h[i], self._w[i])
+                untile(self._pyramid[self._off[i]:self._off[i + 1]], self._rows, self._h[i], self._w[i],
+                       ntx[i])
                 for i in range(self.num_levels)]
         return self._levels_cache
 

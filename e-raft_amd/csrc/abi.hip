@@ -12,24 +12,39 @@
 
 using namespace ecorr;
 
-namespace {
+namespace ecorr {
 
-int layout(int64_t rows, int H, int W, int levels, int* h, int* w, int64_t* off) {
+int pyramid_geometry(int64_t rows, int H, int W, int levels, PyrGeom* g) {
     if (rows <= 0 || H <= 0 || W <= 0) return ECORR_EINVAL;
     if (levels < 1 || levels > ECORR_MAX_LEVELS) return ECORR_ELEVELS;
     int hh = H, ww = W;
     int64_t o = 0;
+    g->levels = levels;
     for (int i = 0; i < levels; ++i) {
         if (i > 0) { hh /= 2; ww /= 2; }
         if (hh == 0 || ww == 0) return ECORR_ESHAPE;
-        if (h) h[i] = hh;
-        if (w) w[i] = ww;
-        if (off) off[i] = o;
-        o += rows * pad_h(hh) * pad_w(ww);   // tiled: each query image padded to 4 x 8 tiles
+        g->h[i] = hh;
+        g->w[i] = ww;
+        if (level_compact(i, hh, ww)) {
+            g->ntx[i] = 0;
+            g->nty[i] = hh;
+            g->sz[i] = (int64_t)hh * ww;
+        } else {
+            g->ntx[i] = pad_w(ww) / kTileW;
+            g->nty[i] = pad_h(hh) / kTileH;
+            g->sz[i] = (int64_t)pad_h(hh) * pad_w(ww);
+        }
+        g->off[i] = o;
+        o += rows * g->sz[i];
+        o = (o + kTile - 1) & ~(int64_t)(kTile - 1);   // every level starts on a 128-byte line
     }
-    if (off) off[levels] = o;
+    g->off[levels] = o;
     return ECORR_OK;
 }
+
+}  // namespace ecorr
+
+namespace {
 
 bool q_count_ok(int H, int W, int q_count) {
     const int64_t Q = (int64_t)H * W;
@@ -61,19 +76,34 @@ ECORR_EXPORT const char* ecorr_strerror(int status) {
 }
 
 ECORR_EXPORT int ecorr_pyramid_layout(int64_t rows, int H, int W, int levels, int* h, int* w, int64_t* off) {
-    return layout(rows, H, W, levels, h, w, off);
+    PyrGeom g;
+    const int st = pyramid_geometry(rows, H, W, levels, &g);
+    if (st != ECORR_OK) return st;
+    for (int i = 0; i < levels; ++i) {
+        if (h) h[i] = g.h[i];
+        if (w) w[i] = g.w[i];
+        if (off) off[i] = g.off[i];
+    }
+    if (off) off[levels] = g.off[levels];
+    return ECORR_OK;
+}
+
+ECORR_EXPORT int ecorr_pyramid_formats(int H, int W, int levels, int* ntx) {
+    if (!ntx) return ECORR_EINVAL;
+    PyrGeom g;
+    const int st = pyramid_geometry(1, H, W, levels, &g);
+    if (st != ECORR_OK) return st;
+    for (int i = 0; i < levels; ++i) ntx[i] = g.ntx[i];
+    return ECORR_OK;
 }
 
 ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
                              int levels, float* pyramid, void* stream) {
     if (!fmap1 || !fmap2 || !pyramid || B <= 0 || D <= 0) return ECORR_EINVAL;
     if (!q_count_ok(H, W, q_count)) return ECORR_EINVAL;
-    int h[ECORR_MAX_LEVELS], w[ECORR_MAX_LEVELS];
-    int64_t off[ECORR_MAX_LEVELS + 1];
-    const int st = layout((int64_t)B * q_count, H, W, levels, h, w, off);
+    PyrGeom g;
+    const int st = pyramid_geometry((int64_t)B * q_count, H, W, levels, &g);
     if (st != ECORR_OK) return st;
-    float* lvl[ECORR_MAX_LEVELS];
-    for (int i = 0; i < levels; ++i) lvl[i] = pyramid + off[i];
 
     BuildParams P{};
     P.f1 = fmap1;
@@ -89,7 +119,7 @@ ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int 
     const float mant = frexpf(s, &e);
     P.scale_is_mul = (mant == 0.5f) ? 1 : 0;
     P.scale = P.scale_is_mul ? 1.0f / s : s;
-    return launch_build(P, B, levels, h, w, lvl, (hipStream_t)stream);
+    return launch_build(P, B, g, pyramid, (hipStream_t)stream);
 }
 
 ECORR_EXPORT int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
@@ -98,13 +128,15 @@ ECORR_EXPORT int ecorr_lookup(const float* pyramid, const float* coords, int B, 
     if (!q_count_ok(H, W, q_count)) return ECORR_EINVAL;
     if (radius < 0 || radius > 32) return ECORR_ERADIUS;
     LookupParams P{};
-    int64_t off[ECORR_MAX_LEVELS + 1];
-    const int st = layout((int64_t)B * q_count, H, W, levels, P.lh, P.lw, off);
+    PyrGeom g;
+    const int st = pyramid_geometry((int64_t)B * q_count, H, W, levels, &g);
     if (st != ECORR_OK) return st;
     for (int i = 0; i < levels; ++i) {
-        P.lvl[i] = pyramid + off[i];
-        P.lntx[i] = pad_w(P.lw[i]) / kTileW;
-        P.lsz[i] = pad_h(P.lh[i]) * pad_w(P.lw[i]);
+        P.lvl[i] = pyramid + g.off[i];
+        P.lh[i] = g.h[i];
+        P.lw[i] = g.w[i];
+        P.lntx[i] = g.ntx[i];
+        P.lsz[i] = (int)g.sz[i];
     }
     P.coords = coords;
     P.out = out;

@@ -157,21 +157,43 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
             }
         }
     }
-    if (P.fused_levels >= 3 && tid < 2 * MR) {   // level 2: rows (ty0/4)&3 + {0,1}, cols (tx0/4)&7 .. +3
-        const int tr = tc.ty0 / 16, tcc = tc.tx0 / 32;
+    if (P.fused_levels >= 3 && tid < 2 * MR) {   // level 2: rows ty0/4 + {0,1}, cols tx0/4 .. +3
         const int mm = tid >> 1, y = tid & 1;
-        if (tr < P.lnty[2] && tcc < P.lntx[2] && mm < mvalid) {
-            const int r = ((tc.ty0 / 4) & 3) + y, c0 = (tc.tx0 / 4) & 7;
-            *reinterpret_cast<floatx4*>(P.lvl[2] + (row0 + mm) * P.lsz[2] + (tr * P.lntx[2] + tcc) * kTile + r * 8 + c0) =
-                *reinterpret_cast<const floatx4*>(S2 + mm * P2S + y * 4);
+        if (mm < mvalid) {
+            const float* src = S2 + mm * P2S + y * 4;
+            float* img = P.lvl[2] + (row0 + mm) * P.lsz[2];
+            if (P.lntx[2] > 0) {
+                const int tr = tc.ty0 / 16, tcc = tc.tx0 / 32;
+                if (tr < P.lnty[2] && tcc < P.lntx[2]) {
+                    const int r = ((tc.ty0 / 4) & 3) + y, c0 = (tc.tx0 / 4) & 7;
+                    *reinterpret_cast<floatx4*>(img + (tr * P.lntx[2] + tcc) * kTile + r * 8 + c0) =
+                        *reinterpret_cast<const floatx4*>(src);
+                }
+            } else {   // compact row-major: no padding cells, so every pixel is range-checked
+                const int r = tc.ty0 / 4 + y, c0 = tc.tx0 / 4;
+                if (r < P.lh[2])
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (c0 + j < P.lw[2]) img[r * P.lw[2] + c0 + j] = src[j];
+            }
         }
     }
-    if (P.fused_levels >= 4 && tid < MR) {   // level 3: row (ty0/8)&3, cols (tx0/8)&7 .. +1
-        const int tr = tc.ty0 / 32, tcc = tc.tx0 / 64;
-        if (tr < P.lnty[3] && tcc < P.lntx[3] && tid < mvalid) {
-            const int r = (tc.ty0 / 8) & 3, c0 = (tc.tx0 / 8) & 7;
-            *reinterpret_cast<floatx2*>(P.lvl[3] + (row0 + tid) * P.lsz[3] + (tr * P.lntx[3] + tcc) * kTile + r * 8 + c0) =
-                *reinterpret_cast<const floatx2*>(S3 + tid * 2);
+    if (P.fused_levels >= 4 && tid < MR && tid < mvalid) {   // level 3: row ty0/8, cols tx0/8 .. +1
+        const float* src = S3 + tid * 2;
+        float* img = P.lvl[3] + (row0 + tid) * P.lsz[3];
+        if (P.lntx[3] > 0) {
+            const int tr = tc.ty0 / 32, tcc = tc.tx0 / 64;
+            if (tr < P.lnty[3] && tcc < P.lntx[3]) {
+                const int r = (tc.ty0 / 8) & 3, c0 = (tc.tx0 / 8) & 7;
+                *reinterpret_cast<floatx2*>(img + (tr * P.lntx[3] + tcc) * kTile + r * 8 + c0) =
+                    *reinterpret_cast<const floatx2*>(src);
+            }
+        } else {
+            const int r = tc.ty0 / 8, c0 = tc.tx0 / 8;
+            if (r < P.lh[3]) {
+                if (c0 < P.lw[3]) img[r * P.lw[3] + c0] = src[0];
+                if (c0 + 1 < P.lw[3]) img[r * P.lw[3] + c0 + 1] = src[1];
+            }
         }
     }
 }
@@ -311,26 +333,29 @@ __global__ __launch_bounds__(256) void pool2_kernel(const float* __restrict__ in
         const int yx = (int)(i - rw * ho * wo);
         const int y = yx / wo, x = yx - y * wo;
         const float* s = in + rw * sz_in;
-        out[rw * sz_out + tiled_off(y, x, ntx_out)] =
-            pool4(s[tiled_off(2 * y, 2 * x, ntx_in)], s[tiled_off(2 * y, 2 * x + 1, ntx_in)],
-                  s[tiled_off(2 * y + 1, 2 * x, ntx_in)], s[tiled_off(2 * y + 1, 2 * x + 1, ntx_in)]);
+        out[rw * sz_out + level_off(y, x, ntx_out, wo)] =
+            pool4(s[level_off(2 * y, 2 * x, ntx_in, w)], s[level_off(2 * y, 2 * x + 1, ntx_in, w)],
+                  s[level_off(2 * y + 1, 2 * x, ntx_in, w)], s[level_off(2 * y + 1, 2 * x + 1, ntx_in, w)]);
     }
 }
 
 }  // namespace
 
-int launch_build(const BuildParams& P0, int B, int levels, const int* lh, const int* lw,
-                 float* const* lvl, hipStream_t stream) {
+int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid, hipStream_t stream) {
     BuildParams P = P0;
+    const int levels = g.levels;
     P.n_ntx = (P.W + TBW - 1) / TBW;
     P.n_nt = P.n_ntx * ((P.H + TBH - 1) / TBH);
     P.n_mt = (P.q_count + BM - 1) / BM;
     P.fused_levels = levels < 4 ? levels : 4;
     for (int i = 0; i < 4; ++i) {
-        P.lvl[i] = i < levels ? lvl[i] : nullptr;
-        P.lntx[i] = i < levels ? pad_w(lw[i]) / kTileW : 0;
-        P.lnty[i] = i < levels ? pad_h(lh[i]) / kTileH : 0;
-        P.lsz[i] = i < levels ? (int64_t)pad_h(lh[i]) * pad_w(lw[i]) : 0;
+        const bool on = i < levels;
+        P.lvl[i] = on ? pyramid + g.off[i] : nullptr;
+        P.lh[i] = on ? g.h[i] : 0;
+        P.lw[i] = on ? g.w[i] : 0;
+        P.lntx[i] = on ? g.ntx[i] : 0;
+        P.lnty[i] = on ? g.nty[i] : 0;
+        P.lsz[i] = on ? g.sz[i] : 0;
     }
     const int64_t ntiles = (int64_t)B * P.n_mt * P.n_nt;
     if (ntiles <= 0 || ntiles > 0x7fffffff) return ECORR_EINVAL;
@@ -341,7 +366,7 @@ int launch_build(const BuildParams& P0, int B, int levels, const int* lh, const 
     P.dev_skip_epilogue = (kskip && atoi(kskip) == 1) ? 1 : 0;
     const bool vec = (P.W % 4 == 0) && (P.q_count % 4 == 0) && ((uintptr_t)P.f1 % 16 == 0) &&
                      ((uintptr_t)P.f2 % 16 == 0);
-    if ((uintptr_t)lvl[0] % 16 != 0) return ECORR_EINVAL;   // tile stores are 16-byte vectors
+    if ((uintptr_t)pyramid % 16 != 0) return ECORR_EINVAL;   // tile stores are 16-byte vectors
     // dev knob for A/B (tools/ab_build.py): ECORR_BUILD_KB32=1 selects the K=32, full-C-tile,
     // 2-blocks-per-CU variant
     const char* kv = getenv("ECORR_BUILD_KB32");
@@ -354,11 +379,10 @@ int launch_build(const BuildParams& P0, int B, int levels, const int* lh, const 
     if (e != hipSuccess) return ECORR_EHIP - (int)e;
     const int64_t rows = (int64_t)B * P.q_count;
     for (int i = 4; i < levels; ++i) {
-        const int64_t n = rows * (lh[i - 1] / 2) * (lw[i - 1] / 2);
+        const int64_t n = rows * g.h[i] * g.w[i];
         const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
-        hipLaunchKernelGGL(pool2_kernel, dim3(grid), dim3(256), 0, stream, lvl[i - 1], lvl[i], rows, lh[i - 1],
-                           lw[i - 1], pad_w(lw[i - 1]) / kTileW, (int64_t)pad_h(lh[i - 1]) * pad_w(lw[i - 1]),
-                           pad_w(lw[i]) / kTileW, (int64_t)pad_h(lh[i]) * pad_w(lw[i]));
+        hipLaunchKernelGGL(pool2_kernel, dim3(grid), dim3(256), 0, stream, pyramid + g.off[i - 1], pyramid + g.off[i],
+                           rows, g.h[i - 1], g.w[i - 1], g.ntx[i - 1], g.sz[i - 1], g.ntx[i], g.sz[i]);
         e = hipGetLastError();
         if (e != hipSuccess) return ECORR_EHIP - (int)e;
     }

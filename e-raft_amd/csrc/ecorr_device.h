@@ -21,6 +21,19 @@ __host__ __device__ __forceinline__ int tiled_off(int y, int x, int ntx) {
 __host__ __device__ __forceinline__ int pad_h(int h) { return (h + kTileH - 1) & ~(kTileH - 1); }
 __host__ __device__ __forceinline__ int pad_w(int w) { return (w + kTileW - 1) & ~(kTileW - 1); }
 
+// Levels >= 2 whose tile padding would exceed half the image (DSEC level 3: 7 x 10 -> 8 x 16) are
+// stored compact row-major instead: the window covers most of such an image, so the padding would
+// only add lines to every lookup's read footprint (tools/lookup_lab.hip: -5% lookup time).
+__host__ __device__ __forceinline__ bool level_compact(int level, int h, int w) {
+    return level >= 2 && 2 * pad_h(h) * pad_w(w) > 3 * h * w;
+}
+
+// Offset of pixel (y, x) in one query image: tiled (ntx = tiles per tile row > 0) or row-major
+// (ntx <= 0, width w).
+__host__ __device__ __forceinline__ int level_off(int y, int x, int ntx, int w) {
+    return ntx > 0 ? tiled_off(y, x, ntx) : y * w + x;
+}
+
 // model/utils.py:11-12 then ATen grid_sampler unnormalize (align_corners=True):
 //   g  = RN(RN(2x / (size-1)) - 1)
 //   ix = RN(RN(g + 1) * ((size-1)/2))
@@ -44,18 +57,18 @@ __device__ __forceinline__ float blend(float vnw, float vne, float vsw, float vs
 
 // Zeros-padding corner fetch by float coordinates (float compare: NaN and +-huge read 0, exactly
 // as ATen's int32-converted masks do).  Used by the generic / fallback paths only.
-// ntx < 0: row-major image (bilinear_sampler); otherwise a tiled pyramid level.
+// ntx <= 0: row-major image (bilinear_sampler, compact levels); otherwise a tiled pyramid level.
 __device__ __forceinline__ float corner(const float* __restrict__ img, int h, int w, float fx, float fy,
-                                        int ntx = -1) {
+                                        int ntx = 0) {
     const bool in = (fx >= 0.0f) & (fx < (float)w) & (fy >= 0.0f) & (fy < (float)h);
     if (!in) return 0.0f;
     const int y = (int)fy, x = (int)fx;
-    return img[ntx < 0 ? (int64_t)y * w + x : (int64_t)tiled_off(y, x, ntx)];
+    return img[ntx <= 0 ? (int64_t)y * w + x : (int64_t)tiled_off(y, x, ntx)];
 }
 
 // One bilinear sample of img[h][w] at pixel coordinates (x, y) (model/utils.py:7-21).
 __device__ __forceinline__ float sample_px(const float* __restrict__ img, int h, int w, float x, float y,
-                                           int ntx = -1) {
+                                           int ntx = 0) {
     const float ix = unnormalize(x, (float)(w - 1), (float)(w - 1) * 0.5f);
     const float iy = unnormalize(y, (float)(h - 1), (float)(h - 1) * 0.5f);
     const float x0 = floorf(ix), y0 = floorf(iy);

@@ -7,6 +7,19 @@
 
 namespace ecorr {
 
+// Pyramid storage geometry (include/ecorr.h), computed once by pyramid_geometry() (abi.hip) and
+// shared by the build and the lookup.
+struct PyrGeom {
+    int levels;
+    int h[ECORR_MAX_LEVELS], w[ECORR_MAX_LEVELS];   // true level sizes
+    int ntx[ECORR_MAX_LEVELS];                       // tiles per tile row; 0 = compact row-major
+    int nty[ECORR_MAX_LEVELS];                       // tile rows (compact: image rows)
+    int64_t sz[ECORR_MAX_LEVELS];                    // floats per query image
+    int64_t off[ECORR_MAX_LEVELS + 1];               // float offset of each level; off[levels] = total
+};
+
+int pyramid_geometry(int64_t rows, int H, int W, int levels, PyrGeom* g);
+
 struct BuildParams {
     const float* f1;
     const float* f2;
@@ -19,12 +32,12 @@ struct BuildParams {
     int fused_levels;   // levels written by the GEMM epilogue (<= 4)
     int dev_skip_epilogue;  // A/B ablation only (ECORR_BUILD_SKIP_EPILOGUE): no pyramid stores
     float* lvl[4];
-    int lntx[4], lnty[4];   // tiles per tile row / tile rows of each fused level
-    int64_t lsz[4];         // floats per query image of each fused level (padded to tiles)
+    int lh[4], lw[4];
+    int lntx[4], lnty[4];   // tiles per tile row (0 = compact row-major) / tile rows of each fused level
+    int64_t lsz[4];         // floats per query image of each fused level
 };
 
-int launch_build(const BuildParams& P, int B, int levels, const int* lh, const int* lw,
-                 float* const* lvl, hipStream_t stream);
+int launch_build(const BuildParams& P, int B, const PyrGeom& g, float* pyramid, hipStream_t stream);
 
 struct LookupParams {
     const float* coords;  // [B][2][q_count]
@@ -35,8 +48,8 @@ struct LookupParams {
     int C;                // levels * (2r+1)^2
     const float* lvl[ECORR_MAX_LEVELS];
     int lh[ECORR_MAX_LEVELS], lw[ECORR_MAX_LEVELS];
-    int lntx[ECORR_MAX_LEVELS];      // tiles per tile row
-    int lsz[ECORR_MAX_LEVELS];       // floats per query image (padded to tiles)
+    int lntx[ECORR_MAX_LEVELS];      // tiles per tile row (0 = compact row-major)
+    int lsz[ECORR_MAX_LEVELS];       // floats per query image
 };
 
 int launch_lookup(const LookupParams& P, int B, hipStream_t stream);

@@ -20,7 +20,7 @@ import torch.distributed as dist
 
 from . import _lib
 from .corr import _no_grad_inputs, _require_device_f32
-from .layout import untile
+from .layout import formats, untile
 
 
 def row_partition(H, world):
@@ -112,8 +112,9 @@ class RowShardedCorrBlock:
         """This rank's levels in the reference layout [B*rows_r*W, 1, h_i, w_i] (a copy)."""
         if self._levels_cache is None:
             rows = self._shape[0] * self.q_count
+            ntx = formats(self._shape[2], self._shape[3], self.num_levels)
             self._levels_cache = [
-                untile(self._pyramid[self._off[i]:self._off[i + 1]], rows, self._h[i], self._w[i])
+                untile(self._pyramid[self._off[i]:self._off[i + 1]], rows, self._h[i], self._w[i], ntx[i])
                 for i in range(self.num_levels)]
         return self._levels_cache
 

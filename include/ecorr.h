@@ -9,16 +9,19 @@
  * C++ exception crosses this boundary.
  *
  * Pyramid storage (what ecorr_build writes, ecorr_lookup reads) -- a layout chosen for the gather:
- * `levels` blocks concatenated at float offsets off_i; level i holds rows = B * q_count query
- * images of h_i x w_i (h_0 = H, w_0 = W, h_{i+1} = h_i / 2, w_{i+1} = w_i / 2, floor -- the
- * shapes of the reference's corr_pyramid[i], corr.py:16-27), each image stored as row-major
- * ECORR_TILE_H x ECORR_TILE_W tiles of 32 floats (128 bytes, one L2 line):
- *   image r of level i starts at off_i + r * hp_i * wp_i, hp_i = roundup(h_i, 4),
- *   wp_i = roundup(w_i, 8), and pixel (y, x) sits at
- *   ((y / 4) * (wp_i / 8) + x / 8) * 32 + (y % 4) * 8 + x % 8.
- * A radius-4 window then touches ~7 lines per level instead of ~13 with row-major images.  Padding
- * cells are never read.  The Python shim materializes reference-layout corr_pyramid views on
- * demand.
+ * `levels` blocks concatenated at float offsets off_i (each a multiple of 32 floats, i.e. 128-byte
+ * aligned); level i holds rows = B * q_count query images of h_i x w_i (h_0 = H, w_0 = W,
+ * h_{i+1} = h_i / 2, w_{i+1} = w_i / 2, floor -- the shapes of the reference's corr_pyramid[i],
+ * corr.py:16-27).  Each image is stored in one of two formats (ecorr_pyramid_formats):
+ *   tiled (ntx_i > 0): row-major ECORR_TILE_H x ECORR_TILE_W tiles of 32 floats (128 bytes, one
+ *     L2 line); image r starts at off_i + r * hp_i * wp_i, hp_i = roundup(h_i, 4),
+ *     wp_i = roundup(w_i, 8) = 8 * ntx_i, and pixel (y, x) sits at
+ *     ((y / 4) * ntx_i + x / 8) * 32 + (y % 4) * 8 + x % 8.  A radius-4 window then touches ~7
+ *     lines per level instead of ~13 with row-major images; padding cells are never read.
+ *   compact (ntx_i = 0): plain row-major h_i x w_i, image r at off_i + r * h_i * w_i.  Used for
+ *     levels i >= 2 whose tile padding would exceed half the image (2 hp wp > 3 h w; DSEC level
+ *     3: 7 x 10), where the window covers most of the image anyway.
+ * The Python shim materializes reference-layout corr_pyramid views on demand.
  *
  * Query slabs (multi-GPU query-row sharding): fmap1, coords and the lookup output hold
  * the q_count query pixels being served -- all H*W of them for the plain CorrBlock, a contiguous
@@ -33,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 3
+#define ECORR_ABI_VERSION 4
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -49,8 +52,8 @@ enum ecorr_status {
 };
 
 /* Layout of the pyramid for `rows` query rows (rows = B * q_count).  Writes h[levels],
- * w[levels] (true level sizes), off[levels + 1] (float offsets including tile padding;
- * off[levels] = total floats).
+ * w[levels] (true level sizes), off[levels + 1] (float offsets including tile padding and the
+ * 128-byte alignment of each level; off[levels] = total floats).
  * Replaces: the shapes produced by CorrBlock.__init__'s reshape + avg_pool2d loop, corr.py:21-27. */
 int ecorr_pyramid_layout(int64_t rows, int H, int W, int levels, int* h, int* w, int64_t* off);
 
@@ -81,6 +84,10 @@ int ecorr_coords_grid(int B, int H, int W, float* out, void* stream);
 
 /* Tile shape of the pyramid storage (ECORR_TILE_H, ECORR_TILE_W). */
 int ecorr_pyramid_tile(int* tile_h, int* tile_w);
+
+/* Storage format of each level of an H x W pyramid: ntx[i] = tiles per tile row (tiled) or 0
+ * (compact row-major).  Same errors as ecorr_pyramid_layout. */
+int ecorr_pyramid_formats(int H, int W, int levels, int* ntx);
 
 /* Human-readable name of a status code (static storage). */
 const char* ecorr_strerror(int status);

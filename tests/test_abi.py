@@ -51,9 +51,17 @@ def test_layout_matches_reference_shapes(ea):
     from eraft_amd import _lib
     h, w, off = _lib.layout(16 * 4800, 60, 80, 4)
     assert (h, w) == ([60, 30, 15, 7], [80, 40, 20, 10])
-    # tiled storage: each image padded to 4 x 8 tiles (60x80, 32x40, 16x24, 8x16)
-    sizes = [60 * 80, 32 * 40, 16 * 24, 8 * 16]
+    # levels 0-2 tiled (each image padded to 4 x 8 tiles: 60x80, 32x40, 16x24); level 3 (7 x 10,
+    # tiles would pad it to 8 x 16) compact row-major; every level starts on a 128-byte line
+    sizes = [60 * 80, 32 * 40, 16 * 24, 7 * 10]
     assert off == [0] + list(np.cumsum([76800 * s for s in sizes]))
+    from eraft_amd.layout import formats
+    assert formats(60, 80, 4) == [10, 5, 3, 0]
+    assert formats(32, 32, 4) == [4, 2, 1, 0]        # MVSEC: 4 x 4 level 3 compact
+    assert formats(92, 160, 4) == [20, 10, 5, 3]     # 1280x720: 11 x 20 level 3 stays tiled
+    _, _, off = _lib.layout(3, 20, 20, 4)            # compact 5x5 / 2x2 levels: starts rounded to 32
+    assert formats(20, 20, 4) == [3, 2, 0, 0]
+    assert off == [0, 1440, 2016, 2112, 2144]
     th, tw = ctypes.c_int(), ctypes.c_int()
     assert ea.lib().ecorr_pyramid_tile(ctypes.byref(th), ctypes.byref(tw)) == 0
     assert (th.value, tw.value) == (4, 8)
@@ -93,10 +101,12 @@ def test_tile_untile_roundtrip():
     from eraft_amd.layout import tile, untile
     for (h, w) in [(60, 80), (15, 20), (7, 10), (1, 1), (9, 11)]:
         lv = torch.arange(3 * h * w, dtype=torch.float32).reshape(3, h, w)
-        flat = tile(lv)
+        flat = tile(lv, ntx=-(-w // 8))
         hp, wp = -(-h // 4) * 4, -(-w // 8) * 8
         assert flat.numel() == 3 * hp * wp
-        assert torch.equal(untile(flat, 3, h, w)[:, 0], lv)
+        assert torch.equal(untile(flat, 3, h, w, ntx=wp // 8)[:, 0], lv)
+        compact = tile(lv, ntx=0)
+        assert torch.equal(compact, lv.reshape(-1)) and torch.equal(untile(compact, 3, h, w, 0)[:, 0], lv)
         # element (y, x) of image r lives at r*hp*wp + ((y//4)*(wp//8) + x//8)*32 + (y%4)*8 + x%8
         r, y, x = 2, h - 1, w - 1
         assert flat[r * hp * wp + ((y // 4) * (wp // 8) + x // 8) * 32 + (y % 4) * 8 + x % 8] == lv[r, y, x]

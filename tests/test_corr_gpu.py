@@ -44,9 +44,9 @@ def ea():
 def _lookup_on(ea, levels, coords, radius):
     """ecorr_lookup on an externally supplied pyramid (list of [N, h, w] numpy levels)."""
     from eraft_amd import _lib
-    from eraft_amd.layout import tile
+    from eraft_amd.layout import pack
     B, _, H, W = coords.shape
-    flat = torch.cat([tile(torch.from_numpy(np.ascontiguousarray(lv))) for lv in levels]).to(DEV)
+    flat = pack([torch.from_numpy(np.ascontiguousarray(lv)) for lv in levels], H, W).to(DEV)
     c = torch.from_numpy(np.ascontiguousarray(coords)).to(DEV)
     K = 2 * radius + 1
     out = torch.empty((B, len(levels) * K * K, H, W), dtype=torch.float32, device=DEV)
