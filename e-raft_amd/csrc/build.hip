@@ -36,9 +36,18 @@ constexpr int NT = 256;           // threads
 constexpr int CS = BN + 4;        // C-tile LDS row stride (floats): conflict-free ds_read_b128
 constexpr int P1S = 36, P2S = 12;  // LDS per-query strides of the pooled staging (conflict-free)
 
-// LDS floats for K chunk KB (double-buffered A and B) and a C tile of MR query rows.
-constexpr int smem_floats(int KB, int MR) {
-    return 2 * (KB * BM + KB * BN) > MR * CS ? 2 * (KB * BM + KB * BN) : MR * CS;
+// LDS floats for K chunk KB (double-buffered A and B, row strides AS / BS) and a C tile of MR
+// query rows.
+constexpr int smem_floats(int KB, int MR, int AS, int BS) {
+    return 2 * (KB * AS + KB * BS) > MR * CS ? 2 * (KB * AS + KB * BS) : MR * CS;
+}
+
+// 16-byte pyramid store; NTS = non-temporal: the 2 GB pyramid is not re-read by this kernel, and
+// streaming it past the caches took 5% off the build (tools/ab_build.py)
+template <bool NTS, typename V>
+__device__ __forceinline__ void st(V* p, V v) {
+    if (NTS) __builtin_nontemporal_store(v, p);
+    else *p = v;
 }
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -49,7 +58,11 @@ __device__ __forceinline__ float pool4(float a, float b, float c, float d) {
     return __fmul_rn(__fadd_rn(__fadd_rn(__fadd_rn(a, b), c), d), 0.25f);
 }
 
-struct TileCoord { int b, m0, ty0, tx0; };
+// A tile covers 128 queries x 128 targets: a TBH x TBW = 8 x 16 target block (regular), or, in the
+// last 4 rows when H % 8 is 1..4, a 4 x 32 block ("band"): those rows feed pyramid levels 0-2 only
+// (level 3 of an H = 8k + r map, r <= 4, has k rows), so the band pools 4 x 8 sub-blocks and no
+// 8-row tile row is padded half empty (DSEC H = 60: 6.7% of the MFMA work saved).
+struct TileCoord { int b, m0, ty0, tx0, band; };
 
 // Grouped tile order (8 m-tiles x all n-tiles per group): consecutive tiles share fmap panels.
 __device__ __forceinline__ TileCoord decode_tile(const BuildParams& P, int t) {
@@ -63,10 +76,17 @@ __device__ __forceinline__ TileCoord decode_tile(const BuildParams& P, int t) {
     const int first_m = grp * GM;
     const int gsm = min(P.n_mt - first_m, GM);
     const int mt = first_m + gi % gsm, nt = gi / gsm;
-    const int nty = nt / P.n_ntx, ntx = nt - nty * P.n_ntx;
     c.m0 = mt * BM;
-    c.ty0 = nty * TBH;
-    c.tx0 = ntx * TBW;
+    if (nt < P.n_reg) {
+        const int nty = nt / P.n_ntx, ntx = nt - nty * P.n_ntx;
+        c.ty0 = nty * TBH;
+        c.tx0 = ntx * TBW;
+        c.band = 0;
+    } else {
+        c.ty0 = P.band_y0;
+        c.tx0 = (nt - P.n_reg) * 32;
+        c.band = 1;
+    }
     return c;
 }
 
@@ -83,7 +103,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // from the rounded previous one, parks levels 1-3 in LDS, then level 1 leaves as one whole tile
 // per query, level 2 as two 16-byte rows, level 3 as 8 bytes.  Tiles beyond a level's padded
 // extent are skipped; padding cells inside a tile are written but never read.
-template <int MR>
+template <int MR, bool NTS>
 __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& tc, float* Cs, int tid, int mlo) {
     // Cs holds C-tile rows [mlo, mlo + MR) of the block's 128 queries
     const int64_t row0 = (int64_t)tc.b * P.q_count + tc.m0 + mlo;
@@ -100,7 +120,7 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
             if (m < mvalid && tr < nty && tcc < ntx) {
                 const floatx4 v = *reinterpret_cast<const floatx4*>(
                     Cs + m * CS + (trl * 4 + (j >> 1)) * TBW + tcl * 8 + (j & 1) * 4);
-                *reinterpret_cast<floatx4*>(P.lvl[0] + (row0 + m) * P.lsz[0] + (tr * ntx + tcc) * kTile + 4 * j) = v;
+                st<NTS>(reinterpret_cast<floatx4*>(P.lvl[0] + (row0 + m) * P.lsz[0] + (tr * ntx + tcc) * kTile + 4 * j), v);
             }
         }
     }
@@ -152,8 +172,8 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
                 const int idx = tid + NT * s;
                 const int mm = idx >> 3, j = idx & 7;
                 if (mm < mvalid)
-                    *reinterpret_cast<floatx4*>(base + (row0 + mm) * P.lsz[1] + 4 * j) =
-                        *reinterpret_cast<const floatx4*>(S1 + mm * P1S + 4 * j);
+                    st<NTS>(reinterpret_cast<floatx4*>(base + (row0 + mm) * P.lsz[1] + 4 * j),
+                            *reinterpret_cast<const floatx4*>(S1 + mm * P1S + 4 * j));
             }
         }
     }
@@ -198,15 +218,114 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
     }
 }
 
+// Epilogue of a band tile (4 target rows x 32 cols; n = ty*32 + tx).  Level 0: one tile row of
+// 4 tiles per query.  Pooling: thread (query m, 4x8 block blk = 0..3) reduces 4x8 -> 2x4 -> 1x2 in
+// registers (the reference's order, from the rounded previous level); level 1 leaves as two 8-float
+// rows of two tiles, level 2 as one 8-float row.  No level-3 pixel draws on these rows.
+template <int MR, bool NTS>
+__device__ __forceinline__ void epilogue_band(const BuildParams& P, const TileCoord& tc, float* Cs, int tid, int mlo) {
+    const int64_t row0 = (int64_t)tc.b * P.q_count + tc.m0 + mlo;
+    const int mvalid = min(MR, P.q_count - tc.m0 - mlo);
+    {   // level 0: tile row ty0/4, tile cols tx0/8 .. +3
+        const int ntx = P.lntx[0];
+        const int tr = tc.ty0 / kTileH, tc0 = tc.tx0 / kTileW;
+#pragma unroll 4
+        for (int s = 0; s < (MR * 32) / NT; ++s) {
+            const int idx = tid + NT * s;
+            const int m = idx >> 5, rem = idx & 31;
+            const int tcl = rem >> 3, j = rem & 7;
+            if (m < mvalid && tc0 + tcl < ntx) {
+                const floatx4 v = *reinterpret_cast<const floatx4*>(Cs + m * CS + (j >> 1) * 32 + tcl * 8 + (j & 1) * 4);
+                st<NTS>(reinterpret_cast<floatx4*>(P.lvl[0] + (row0 + m) * P.lsz[0] + (tr * ntx + tc0 + tcl) * kTile + 4 * j), v);
+            }
+        }
+    }
+    if (P.fused_levels < 2) return;
+    constexpr int NU = (4 * MR + NT - 1) / NT;   // (query, block) items per thread
+    float l1[NU][2][4], l2[NU][2];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int it = tid + NT * u, m = it % MR, blk = it / MR;
+        if (it < 4 * MR) {
+            float v[4][8];
+#pragma unroll
+            for (int ty = 0; ty < 4; ++ty) {
+                const floatx4 lo = *reinterpret_cast<const floatx4*>(Cs + m * CS + ty * 32 + blk * 8);
+                const floatx4 hi = *reinterpret_cast<const floatx4*>(Cs + m * CS + ty * 32 + blk * 8 + 4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { v[ty][j] = lo[j]; v[ty][4 + j] = hi[j]; }
+            }
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+                    l1[u][y][x] = pool4(v[2 * y][2 * x], v[2 * y][2 * x + 1], v[2 * y + 1][2 * x], v[2 * y + 1][2 * x + 1]);
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+                l2[u][x] = pool4(l1[u][0][2 * x], l1[u][0][2 * x + 1], l1[u][1][2 * x], l1[u][1][2 * x + 1]);
+        }
+    }
+    __syncthreads();   // all reads of Cs done: reuse it for the pooled staging
+    float* S1 = Cs;                 // [MR][2 rows][16 cols], stride P1S
+    float* S2 = Cs + MR * P1S;      // [MR][8 cols], stride P2S
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int it = tid + NT * u, m = it % MR, blk = it / MR;
+        if (it < 4 * MR) {
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+                *reinterpret_cast<floatx4*>(S1 + m * P1S + y * 16 + blk * 4) =
+                    floatx4{l1[u][y][0], l1[u][y][1], l1[u][y][2], l1[u][y][3]};
+            *reinterpret_cast<floatx2*>(S2 + m * P2S + blk * 2) = floatx2{l2[u][0], l2[u][1]};
+        }
+    }
+    __syncthreads();
+    {   // level 1: rows ty0/2 .. +1 (in-tile rows 0-1 of tile row ty0/8), tile cols tx0/16 .. +1
+        const int tr = tc.ty0 / 8, tc0 = tc.tx0 / 16;
+        if (tr < P.lnty[1]) {
+#pragma unroll
+            for (int s = 0; s < (MR * 8 + NT - 1) / NT; ++s) {
+                const int idx = tid + NT * s;
+                const int mm = idx >> 3, t = idx & 7;
+                const int y = t >> 2, tcl = (t >> 1) & 1, hf = t & 1;
+                if (mm < mvalid && tc0 + tcl < P.lntx[1])
+                    st<NTS>(reinterpret_cast<floatx4*>(P.lvl[1] + (row0 + mm) * P.lsz[1] +
+                                                       (tr * P.lntx[1] + tc0 + tcl) * kTile + y * 8 + hf * 4),
+                            *reinterpret_cast<const floatx4*>(S1 + mm * P1S + y * 16 + tcl * 8 + hf * 4));
+            }
+        }
+    }
+    if (P.fused_levels >= 3 && tid < 2 * MR) {   // level 2: row ty0/4, cols tx0/4 .. +7
+        const int mm = tid >> 1, hf = tid & 1;
+        if (mm < mvalid) {
+            const float* src = S2 + mm * P2S + hf * 4;
+            float* img = P.lvl[2] + (row0 + mm) * P.lsz[2];
+            const int r = tc.ty0 / 4, c0 = tc.tx0 / 4 + hf * 4;
+            if (P.lntx[2] > 0) {
+                const int tr = r / 4, tcc = c0 / 8;
+                if (tr < P.lnty[2] && tcc < P.lntx[2])
+                    *reinterpret_cast<floatx4*>(img + (tr * P.lntx[2] + tcc) * kTile + (r & 3) * 8 + (c0 & 7)) =
+                        *reinterpret_cast<const floatx4*>(src);
+            } else if (r < P.lh[2]) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (c0 + j < P.lw[2]) img[r * P.lw[2] + c0 + j] = src[j];
+            }
+        }
+    }
+}
+
 // KB = K chunk depth; HALF = C tile handled in two 64-query halves.  KB = 16 + HALF needs 34 KB of
 // LDS and <= 168 VGPRs, so 3 blocks (3 waves per SIMD) share a CU; KB = 32 uses 67.5 KB (2 blocks).
-template <bool VEC, int KB, bool HALF>
+// (A/B: v_mfma_f32_16x16x4_f32 tiles, bitwise the same result, ran 1% slower than 32x32x2.)
+template <bool VEC, int KB, bool HALF, bool NTS>
 __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) {
     constexpr int MR = HALF ? BM / 2 : BM;
+    constexpr int AS = BM, BSS = BN;   // LDS row strides
     constexpr int NLD = (KB * BM / 4) / NT;   // float4 of A (and of B) per thread per chunk
-    __shared__ __attribute__((aligned(16))) float smem[smem_floats(KB, MR)];
-    float* As = smem;                       // [2][KB][BM]
-    float* Bs = smem + 2 * KB * BM;         // [2][KB][BN]
+    __shared__ __attribute__((aligned(16))) float smem[smem_floats(KB, MR, AS, BSS)];
+    float* As = smem;                       // [2][KB][AS]
+    float* Bs = smem + 2 * KB * AS;         // [2][KB][BSS]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TileCoord tc = decode_tile(P, xcd_remap(blockIdx.x, gridDim.x));
@@ -236,8 +355,9 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                 }
                 ra[i] = v;
             }
-            {   // B: row k, target row ty0 + ty, cols tx0 + 4c .. +3
-                const int r = s & 31, y = tc.ty0 + (r >> 2), x = tc.tx0 + 4 * (r & 3);
+            {   // B: row k, target row ty0 + ty, cols tx0 + 4c .. +3 (LDS column 4r = ty*TBW + tx)
+                const int r = s & 31;
+                const int y = tc.ty0 + (tc.band ? r >> 3 : r >> 2), x = tc.tx0 + 4 * (tc.band ? r & 7 : r & 3);
                 floatx4 v = {0.f, 0.f, 0.f, 0.f};
                 if (VEC) {
                     if (k < D && y < H && x < W)
@@ -256,8 +376,8 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
         for (int i = 0; i < NLD; ++i) {
             const int s = tid + NT * i;
             const int kk = s >> 5, c = s & 31;
-            *reinterpret_cast<floatx4*>(As + (buf * KB + kk) * BM + 4 * c) = ra[i];
-            *reinterpret_cast<floatx4*>(Bs + (buf * KB + kk) * BN + 4 * c) = rb[i];
+            *reinterpret_cast<floatx4*>(As + (buf * KB + kk) * AS + 4 * c) = ra[i];
+            *reinterpret_cast<floatx4*>(Bs + (buf * KB + kk) * BSS + 4 * c) = rb[i];
         }
     };
 
@@ -280,13 +400,13 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
     for (int kc = 0; kc < nk; ++kc) {
         const int buf = kc & 1;
         if (kc + 1 < nk) load_chunk((kc + 1) * KB);
-        const float* as = As + buf * KB * BM + wm * 64 + acol;
-        const float* bs = Bs + buf * KB * BN + wn * 64 + acol;
+        const float* as = As + buf * KB * AS + wm * 64 + acol;
+        const float* bs = Bs + buf * KB * BSS + wn * 64 + acol;
 #pragma unroll
         for (int kk = 0; kk < KB; kk += 2) {
             const int ro = kk + arow;
-            const float a0 = as[ro * BM], a1 = as[ro * BM + 32];
-            const float b0 = bs[ro * BN], b1 = bs[ro * BN + 32];
+            const float a0 = as[ro * AS], a1 = as[ro * AS + 32];
+            const float b0 = bs[ro * BSS], b1 = bs[ro * BSS + 32];
             acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
             acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
             acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
@@ -302,13 +422,14 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
 #pragma unroll
     for (int half = 0; half < (HALF ? 2 : 1); ++half) {
         if (!HALF || wm == half) {
+            const int mb = HALF ? 0 : wm * 64;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        const int m = (HALF ? 0 : wm * 64) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
+                        const int m = mb + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
                         const int n = wn * 64 + j * 32 + acol;
                         const float v = acc[i][j][r];
                         Cs[m * CS + n] = P.scale_is_mul ? __fmul_rn(v, P.scale) : __fdiv_rn(v, P.scale);
@@ -316,7 +437,8 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
         }
         __syncthreads();
         if (P.dev_skip_epilogue) continue;
-        epilogue<MR>(P, tc, Cs, tid, half * MR);
+        if (tc.band) epilogue_band<MR, NTS>(P, tc, Cs, tid, half * MR);
+        else epilogue<MR, NTS>(P, tc, Cs, tid, half * MR);
         if (HALF && half == 0) __syncthreads();   // half 0 fully consumed before half 1 overwrites Cs
     }
 }
@@ -344,10 +466,17 @@ __global__ __launch_bounds__(256) void pool2_kernel(const float* __restrict__ in
 int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid, hipStream_t stream) {
     BuildParams P = P0;
     const int levels = g.levels;
-    P.n_ntx = (P.W + TBW - 1) / TBW;
-    P.n_nt = P.n_ntx * ((P.H + TBH - 1) / TBH);
-    P.n_mt = (P.q_count + BM - 1) / BM;
     P.fused_levels = levels < 4 ? levels : 4;
+    P.n_ntx = (P.W + TBW - 1) / TBW;
+    // 8-row tile rows; a remainder of 1..4 rows (the last 8k + r rows, r <= 4) becomes a band of
+    // 4 x 32 tiles (see TileCoord), a remainder of 5..7 a padded regular tile row
+    const int rem = P.H % TBH;
+    // dev knob for A/B (tools/ab_build.py): ECORR_BUILD_NOBAND=1 pads the remainder instead
+    const bool band = rem > 0 && rem <= 4 && getenv("ECORR_BUILD_NOBAND") == nullptr;
+    P.n_reg = P.n_ntx * (band ? P.H / TBH : (P.H + TBH - 1) / TBH);
+    P.band_y0 = (P.H / TBH) * TBH;
+    P.n_nt = P.n_reg + (band ? (P.W + 31) / 32 : 0);
+    P.n_mt = (P.q_count + BM - 1) / BM;
     for (int i = 0; i < 4; ++i) {
         const bool on = i < levels;
         P.lvl[i] = on ? pyramid + g.off[i] : nullptr;
@@ -372,9 +501,9 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
     const char* kv = getenv("ECORR_BUILD_KB32");
     const bool kb32 = kv && atoi(kv) == 1;
     const dim3 grid((unsigned)ntiles), block(NT);
-    if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true>), grid, block, 0, stream, P);
-    else if (kb32) hipLaunchKernelGGL((build_kernel<true, 32, false>), grid, block, 0, stream, P);
-    else hipLaunchKernelGGL((build_kernel<true, 16, true>), grid, block, 0, stream, P);
+    if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true>), grid, block, 0, stream, P);
+    else if (kb32) hipLaunchKernelGGL((build_kernel<true, 32, false, true>), grid, block, 0, stream, P);
+    else hipLaunchKernelGGL((build_kernel<true, 16, true, true>), grid, block, 0, stream, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ECORR_EHIP - (int)e;
     const int64_t rows = (int64_t)B * P.q_count;

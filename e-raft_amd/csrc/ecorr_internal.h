@@ -29,6 +29,7 @@ struct BuildParams {
     int scale_is_mul;
     // filled by launch_build
     int n_mt, n_nt, n_ntx, n_tiles;
+    int n_reg, band_y0;  // regular (8 x 16) n-tiles per m-tile; first row of the 4-row band tiles
     int fused_levels;   // levels written by the GEMM epilogue (<= 4)
     int dev_skip_epilogue;  // A/B ablation only (ECORR_BUILD_SKIP_EPILOGUE): no pyramid stores
     float* lvl[4];

@@ -174,3 +174,34 @@ def test_errors_match_reference(ea):
     g = torch.zeros(1, 16, 8, 8, device=DEV, requires_grad=True)
     with pytest.raises(RuntimeError):
         ea.CorrBlock(g, g)
+
+
+# Tile-geometry sweep: H % 8 = 0..7 (regular 8 x 16 tiles, 4 x 32 band tiles for remainders 1-4,
+# padded tile rows for 5-7), widths that are / are not multiples of 4, 16 and 32 (vector and
+# scalar loaders, partial band tiles), 1..5 levels (levels >= 4 pooled by pool2_kernel), tiled
+# and compact level formats.
+GEOMETRY = [(1, 32, 60, 80, 4), (1, 16, 17, 20, 4), (2, 16, 19, 24, 3), (1, 8, 20, 36, 4),
+            (1, 8, 21, 40, 2), (1, 16, 22, 18, 4), (1, 8, 23, 16, 1), (1, 16, 24, 44, 4),
+            (1, 8, 25, 33, 4), (2, 16, 36, 52, 5), (1, 8, 12, 100, 4), (1, 16, 92, 160, 4)]
+
+
+@pytest.mark.parametrize("geom", GEOMETRY, ids=lambda g: "b%d_d%d_%dx%d_l%d" % g)
+def test_geometry_vs_oracle(ea, geom):
+    B, D, H, W, L = geom
+    f1, f2 = prng.normal(21, (B, D, H, W)), prng.normal(22, (B, D, H, W))
+    coords = prng.coords_with_flow(23, B, H, W, 2.5)
+    with torch.no_grad():
+        blk = ea.CorrBlock(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L)
+        out = blk(torch.from_numpy(coords).to(DEV)).cpu().numpy()
+    levels = [lv[:, 0].cpu().numpy() for lv in blk.corr_pyramid]
+    if H * W <= 2500:
+        assert oracle.normwise_err(levels[0], oracle.corr_level0(f1, f2)) <= GEMM_TOL
+    else:   # sampled query rows at the larger shapes
+        for rw in range(0, B * H * W, 613):
+            b, p = divmod(rw, H * W)
+            ref = oracle.corr_level0(f1[b:b + 1], f2[b:b + 1], p, 1)[0]
+            assert oracle.normwise_err(levels[0][rw], ref) <= GEMM_TOL
+    ref_levels = oracle.pyramid_from_level0(levels[0], L)
+    for i in range(1, L):
+        assert oracle.same_bits(levels[i], ref_levels[i]), f"level {i}"
+    assert oracle.same_bits(out, oracle.lookup(levels, coords, 4))

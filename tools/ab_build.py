@@ -12,11 +12,12 @@ sys.path.insert(0, ROOT)
 import eraft_amd  # noqa: E402
 
 VARIANTS = {
-    "kb16_half": {},
-    "kb32_full": {"ECORR_BUILD_KB32": "1"},
-    "kb16_noepi": {"ECORR_BUILD_SKIP_EPILOGUE": "1"},
+    "default": {},
+    "noband": {"ECORR_BUILD_NOBAND": "1"},
+    "kb32": {"ECORR_BUILD_KB32": "1"},
+    "noepi": {"ECORR_BUILD_SKIP_EPILOGUE": "1"},
 }
-KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32")
+KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32", "ECORR_BUILD_NOBAND")
 B = int(os.environ.get("AB_BATCH", "16"))
 H, W, D = 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)
@@ -41,7 +42,7 @@ with torch.no_grad():
                 if ref is None:
                     ref = blk.corr_pyramid[0][:4096].clone()
                 err = (blk.corr_pyramid[0][:4096] - ref).abs().max().item()
-                print(f"{name}: level-0 max |diff| vs first variant {err:.3g}")
+                print(f"{name}: level-0 max |diff| vs first variant {err:.3g}", flush=True)
             for _ in range(3):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
