@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-next", action="store_true", help="skip the SURVEY §8f next-row measurements")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     a = ap.parse_args()
     if a.mode == "batch":
@@ -115,6 +116,39 @@ def cpu_baseline(B, D, H, W, iters, seconds):
     return {"value": pairs / el, "unit": "pairs/s", "cores": cores, "kind": "port",
             "sample": f"{pairs} pairs ({nb} per step, fmap {D}x{H}x{W}, build + {iters} lookups) in "
                       f"{el:.1f} s; torch {torch.__version__} CPU ops = the reference's ATen ops"}
+
+
+def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
+    """fused lookup + convc1 + ReLU (ecorr_lookup_conv1x1_relu) against the
+    unfused path it replaces (our lookup, then torch's conv2d + relu on MIOpen), 12 iterations,
+    HIP events on the launch stream; outside the headline timed region."""
+    import torch.nn.functional as F
+    g = torch.Generator(device=device).manual_seed(99)
+    wgt = torch.randn((256, 324, 1, 1), generator=g, device=device) * 0.05
+    bias = torch.randn((256,), generator=g, device=device) * 0.1
+    stream = torch.cuda.current_stream(device)
+
+    def run(fn):
+        ts = []
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for c in coords:
+                fn(c)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / len(coords))
+        return sorted(ts[1:])[len(ts[1:]) // 2]
+
+    with torch.no_grad():
+        fused = run(lambda c: blk.lookup_conv1x1_relu(c, wgt, bias))
+        unfused = run(lambda c: torch.relu(F.conv2d(blk(c), wgt, bias)))
+    flops = 2.0 * B * H * W * 256 * 324
+    return {"fused_ms_per_iter": round(fused, 4), "unfused_ms_per_iter": round(unfused, 4),
+            "speedup": round(unfused / fused, 3), "bound": "mfma",
+            "achieved": round(flops / (fused * 1e-3) / 1e12, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(flops / (fused * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
+            "work_per_launch": f"{flops:.4g} flop (1x1 conv 324->256 over B*H*W queries)"}
 
 
 def pmc_traffic(kernel_prefix):
@@ -248,6 +282,9 @@ def main():
         "config": cfg, "roofline": roof, "kernels": kernels,
         "corrblock_frac": round(ideal_s / (elapsed / a.steps), 4),
     }
+    if a.mode == "batch" and world == 1 and not a.no_next:
+        with torch.no_grad():
+            res["next_rows"] = {"lookup_conv1x1_relu": measure_fused_convc1(make_block(), coords, B, H, W, device)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(B, D, H, W, iters, a.cpu_seconds)
     if rank == 0:

@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -38,6 +38,8 @@ SYMBOLS = {
     "ecorr_build": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
     # (pyramid, coords, B, H, W, q_count, levels, radius, out, stream)
     "ecorr_lookup": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
+    # (pyramid, coords, B, H, W, q_count, levels, radius, weight[O][C], bias, O, out, stream)
+    "ecorr_lookup_conv1x1_relu": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _p, _p]),
     "ecorr_bilinear_sampler": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _p]),
     "ecorr_coords_grid": (_i, [_i, _i, _i, _p, _p]),
     "ecorr_pyramid_tile": (_i, [ctypes.POINTER(_i), ctypes.POINTER(_i)]),

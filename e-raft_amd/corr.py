@@ -97,6 +97,37 @@ class CorrBlock:
                 self.radius, out.data_ptr(), _lib.stream_of(coords)), "CorrBlock lookup")
         return out
 
+    def lookup_conv1x1_relu(self, coords, weight, bias=None):
+        """F.relu(conv1x1(self(coords), weight, bias)) without materializing the lookup: the
+        lookup fused with BasicMotionEncoder.convc1 + ReLU (update.py:67,74).
+        weight: [O, C, 1, 1] (or [O, C]) fp32 with C = num_levels * (2r+1)^2; bias: [O] or None.
+        Returns [B, O, H, W].  Needs radius 4, num_levels <= 4 and O a multiple of 64."""
+        B, _, H, W = self._shape
+        _require_device_f32("coords", coords)
+        _require_device_f32("weight", weight)
+        _no_grad_inputs(coords, weight, *(() if bias is None else (bias,)))
+        if tuple(coords.shape) != (B, 2, H, W):
+            raise RuntimeError(f"coords shape {tuple(coords.shape)} != {(B, 2, H, W)} of the pyramid")
+        K = 2 * self.radius + 1
+        C = self.num_levels * K * K
+        O = weight.shape[0]
+        if weight.numel() != O * C:
+            raise RuntimeError(f"weight {tuple(weight.shape)} does not map {C} correlation channels")
+        if bias is not None:
+            _require_device_f32("bias", bias)
+            if bias.numel() != O:
+                raise RuntimeError(f"bias has {bias.numel()} elements, expected {O}")
+            bias = bias.contiguous()
+        wt = weight.reshape(O, C).contiguous()   # the conv weight [O, C, 1, 1] as is
+        coords = coords.contiguous()
+        with torch.cuda.device(self._device):
+            out = torch.empty((B, O, H, W), dtype=torch.float32, device=self._device)
+            _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu(
+                self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, self.num_levels,
+                self.radius, wt.data_ptr(), None if bias is None else bias.data_ptr(), O,
+                out.data_ptr(), _lib.stream_of(coords)), "CorrBlock lookup+conv1x1+relu")
+        return out
+
     @staticmethod
     def corr(fmap1, fmap2):
         """Level-0 volume fmap1^T fmap2 / sqrt(D) as [B, H, W, 1, H, W] (corr.py:52-60)."""

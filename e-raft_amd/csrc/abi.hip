@@ -122,32 +122,53 @@ ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int 
     return launch_build(P, B, g, pyramid, (hipStream_t)stream);
 }
 
-ECORR_EXPORT int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
-                              int levels, int radius, float* out, void* stream) {
+namespace {
+
+int lookup_params(const float* pyramid, const float* coords, int B, int H, int W, int q_count, int levels,
+                  int radius, float* out, LookupParams* P) {
     if (!pyramid || !coords || !out || B <= 0) return ECORR_EINVAL;
     if (!q_count_ok(H, W, q_count)) return ECORR_EINVAL;
     if (radius < 0 || radius > 32) return ECORR_ERADIUS;
-    LookupParams P{};
     PyrGeom g;
     const int st = pyramid_geometry((int64_t)B * q_count, H, W, levels, &g);
     if (st != ECORR_OK) return st;
     for (int i = 0; i < levels; ++i) {
-        P.lvl[i] = pyramid + g.off[i];
-        P.lh[i] = g.h[i];
-        P.lw[i] = g.w[i];
-        P.lntx[i] = g.ntx[i];
-        P.lsz[i] = (int)g.sz[i];
+        P->lvl[i] = pyramid + g.off[i];
+        P->lh[i] = g.h[i];
+        P->lw[i] = g.w[i];
+        P->lntx[i] = g.ntx[i];
+        P->lsz[i] = (int)g.sz[i];
     }
-    P.coords = coords;
-    P.out = out;
-    P.H = H;
-    P.W = W;
-    P.q_count = q_count;
-    P.levels = levels;
-    P.radius = radius;
-    P.C = levels * (2 * radius + 1) * (2 * radius + 1);
-    if ((int64_t)B * P.C > 0xffff * 64) return ECORR_EINVAL;
+    P->coords = coords;
+    P->out = out;
+    P->H = H;
+    P->W = W;
+    P->q_count = q_count;
+    P->levels = levels;
+    P->radius = radius;
+    P->C = levels * (2 * radius + 1) * (2 * radius + 1);
+    if ((int64_t)B * P->C > 0xffff * 64) return ECORR_EINVAL;
+    return ECORR_OK;
+}
+
+}  // namespace
+
+ECORR_EXPORT int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
+                              int levels, int radius, float* out, void* stream) {
+    LookupParams P{};
+    const int st = lookup_params(pyramid, coords, B, H, W, q_count, levels, radius, out, &P);
+    if (st != ECORR_OK) return st;
     return launch_lookup(P, B, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_lookup_conv1x1_relu(const float* pyramid, const float* coords, int B, int H, int W,
+                                           int q_count, int levels, int radius, const float* weight,
+                                           const float* bias, int O, float* out, void* stream) {
+    if (!weight) return ECORR_EINVAL;
+    LookupParams P{};
+    const int st = lookup_params(pyramid, coords, B, H, W, q_count, levels, radius, out, &P);
+    if (st != ECORR_OK) return st;
+    return launch_lookup_conv(P, B, weight, bias, O, out, (hipStream_t)stream);
 }
 
 ECORR_EXPORT int ecorr_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,

@@ -6,20 +6,15 @@
 // bit-exact with the reference on CPU (same fp32 op sequence, ecorr_device.h).
 //
 // The lookup is an HBM-bound gather: each query reads its own (2r+2)^2 window per level and
-// nothing is shared between queries.  Design (one workgroup = 64 consecutive queries x 1 level):
-//   phase 0  the 2(2r+1) coordinate chains per query (x chains depend on a only, y chains on b
-//            only, so 18 instead of 162 chains at r=4) -> floor + fraction into LDS;
-//   phase 1  cooperative staging of each query's (2r+3)^2 window (one slack row/column absorbs
-//            the +-1 floor flips of the unnormalize round trip) into LDS, zero-filled outside the
-//            image, with clamped (always valid) addresses;
-//   phase 2  every output from LDS; lanes = 64 consecutive queries so each channel store is one
-//            256-byte coalesced row of the NCHW output, stored non-temporally.
-// Queries whose floors do not fit the staged window (NaN/inf/huge coordinates) take an exact
-// direct-gather path inside phase 2.
+// nothing is shared between queries.  One workgroup = 64 consecutive queries x 1 level; the
+// window staging (phases 0-1) is lookup_stage.h; phase 2 writes every output from LDS with lanes
+// = 64 consecutive queries, so each channel store is one 256-byte coalesced row of the NCHW
+// output, stored non-temporally.
 #include <stdlib.h>
 
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
+#include "lookup_stage.h"
 
 namespace ecorr {
 
@@ -29,134 +24,23 @@ constexpr int NT = 256;   // threads of the generic kernels
 
 // QB queries per workgroup, 4 threads per query (NTQ = 4 * QB threads); QB = 64 -> 4 waves,
 // QB = 16 -> one wave per workgroup (no cross-wave barrier; waves overlap phases freely).
+// LDS ~40 KB, so 4 blocks fit a CU.
 template <int R, int QB>
 __global__ __launch_bounds__(4 * QB) void lookup_staged(LookupParams P) {
     constexpr int NTQ = 4 * QB;
-    constexpr int K = 2 * R + 1;   // samples per axis
-    constexpr int KK = K * K;
-    constexpr int S = 2 * R + 3;   // staged window side
-    constexpr int SS = S * S;
-    constexpr int SP = SS | 1;     // odd per-query stride: conflict-free lanes = queries
-    __shared__ float win[QB * SP];
-    __shared__ float fx[QB][K], wx[QB][K], fy[QB][K], wy[QB][K];
-    // per query: window origin x, y and (mode | needed cols << 8 | needed rows << 16), where mode
-    // 0 = staged, 1 = direct gather (coordinates that do not fit the window), 2 = past the range.
-    // Kept at 40 KB of LDS in total so 4 blocks fit a CU.
-    __shared__ int org[QB][3];
-
-    const int tid = threadIdx.x, g = tid & (QB - 1), part = tid / QB;
+    using WS = WindowStage<R, QB>;
+    __shared__ WS st;
+    const int tid = threadIdx.x, g = tid % QB, part = tid / QB;
     const int lv = blockIdx.y, b = blockIdx.z;
-    const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
-    const int q0 = blockIdx.x * QB;                 // first query of the block (in the slab)
-    const int p = q0 + g;
-    const bool valid = p < P.q_count;
-    const int64_t Q = P.q_count;                    // coords slab stride
-    const int64_t hw = P.lsz[lv];                   // floats per query image (tiled, padded)
-    const float* __restrict__ lvbase = P.lvl[lv] + ((int64_t)b * P.q_count + q0) * hw;
-
-    // ---- phase 0: coordinate chains (corr.py:41-43, utils.py:11-12, grid_sampler unnormalize)
-    if (valid) {
-        const float inv = 1.0f / (float)(1 << lv);  // coords / 2**i is an exact scaling
-        const float cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
-        const float cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);
-        const float wm1 = (float)(w - 1), hm1 = (float)(h - 1);
-#pragma unroll
-        for (int j = part; j < 2 * K; j += 4) {
-            const bool isx = j < K;
-            const int o = isx ? j : j - K;
-            const float c = __fadd_rn(isx ? cx : cy, (float)(o - R));
-            const float m1 = isx ? wm1 : hm1;
-            const float v = unnormalize(c, m1, m1 * 0.5f);
-            const float f = floorf(v);
-            if (isx) { fx[g][o] = f; wx[g][o] = __fsub_rn(v, f); }
-            else     { fy[g][o] = f; wy[g][o] = __fsub_rn(v, f); }
-        }
-    }
-    __syncthreads();
-
-    // ---- phase 0b: window origin and fast/slow decision per query
-    if (part == 0) {
-        int md = 2, X0 = 0, Y0 = 0, NX = 0, NY = 0;
-        if (valid) {
-            const float x0 = fx[g][0], y0 = fy[g][0];
-            bool ok = fabsf(x0) < 1.0e7f && fabsf(y0) < 1.0e7f;  // false for NaN / inf / huge
-#pragma unroll
-            for (int o = 0; o < K; ++o) {
-                const float dx = fx[g][o] - x0, dy = fy[g][o] - y0;  // exact: integers < 2^24
-                ok &= (dx >= 0.0f) & (dx <= (float)(S - 2)) & (dy >= 0.0f) & (dy <= (float)(S - 2));
-            }
-            md = ok ? 0 : 1;
-            X0 = ok ? (int)x0 : 0;
-            Y0 = ok ? (int)y0 : 0;
-            // corners span [x0, floor(ix_last) + 1]: monotone round trip, so the last sample bounds it
-            NX = ok ? (int)(fx[g][K - 1] - x0) + 2 : 0;
-            NY = ok ? (int)(fy[g][K - 1] - y0) + 2 : 0;
-        }
-        org[g][0] = X0;
-        org[g][1] = Y0;
-        org[g][2] = md | (NX << 8) | (NY << 16);
-    }
-    __syncthreads();
-
-    // ---- phase 1: stage windows, zeros outside the image (grid_sample padding_mode='zeros').
-    // Work item = (query, window column); each item walks the S rows.  Loads are raw buffer loads
-    // over this block's slab of the level: an element outside the image gets an out-of-range
-    // offset and the hardware range check returns 0 -- zero padding with no branch and no select,
-    // so all NCOL*S loads of a thread issue back to back.
-    constexpr int ITEMS = QB * S;
-    constexpr int NCOL = (ITEMS + NTQ - 1) / NTQ;
-    const int nq = min(QB, P.q_count - q0);
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lvbase), 0, (int)(nq * hw * 4), 0x00020000);
-    constexpr int OOB = 0x7ffffff0;   // beyond any slab: reads as 0
-    float vals[NCOL][S];
-    int dst[NCOL];
-#pragma unroll
-    for (int c = 0; c < NCOL; ++c) {
-        const int it = tid + c * NTQ;
-        const bool live = it < ITEMS;
-        const int gq = live ? it / S : 0;
-        const int rx = it - gq * S;
-        const int x = org[gq][0] + rx, y0 = org[gq][1], info = org[gq][2];
-        const int ny = (info >> 16) & 0xff;
-        // only the needed corner rectangle touches memory; the slack row/column reads 0 for free
-        const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) && (unsigned)x < (unsigned)w;
-        const int base = (int)(gq * hw);
-        dst[c] = live ? gq * SP + rx : -1;
-#pragma unroll
-        for (int ry = 0; ry < S; ++ry) {
-            const int y = y0 + ry;
-            const int off = (colin && ry < ny && (unsigned)y < (unsigned)h) ? (base + level_off(y, x, ntx, w)) * 4 : OOB;
-            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < NCOL; ++c)
-        if (dst[c] >= 0)
-#pragma unroll
-            for (int ry = 0; ry < S; ++ry) win[dst[c] + ry * S] = vals[c][ry];
-    __syncthreads();
+    const int q0 = blockIdx.x * QB;   // first query of the block (in the slab)
+    stage_level<R, QB, NTQ>(st, P, lv, b, q0, tid);
 
     // ---- phase 2: outputs; lanes = queries -> coalesced channel-row stores
-    const int md = org[g][2] & 0xff;
+    const int md = st.org[g][2] & 0xff;
     if (md == 2) return;
-    float* __restrict__ outp = P.out + ((int64_t)b * P.C + (int64_t)lv * KK) * P.q_count + q0 + g;
-    const int X0 = org[g][0], Y0 = org[g][1];
-    const float* wq = win + g * SP;
-    const float* img = lvbase + (int64_t)g * hw;
-    for (int k = part; k < KK; k += 4) {
-        const int a = k / K, bb = k - a * K;
-        const float xa = fx[g][a], yb = fy[g][bb];
-        const float wa = wx[g][a], nb = wy[g][bb];
-        float res;
-        if (md == 0) {
-            const float* c = wq + ((int)yb - Y0) * S + ((int)xa - X0);
-            res = blend(c[0], c[1], c[S], c[S + 1], wa, nb);
-        } else {
-            const float xa1 = __fadd_rn(xa, 1.0f), yb1 = __fadd_rn(yb, 1.0f);
-            res = blend(corner(img, h, w, xa, yb, ntx), corner(img, h, w, xa1, yb, ntx),
-                        corner(img, h, w, xa, yb1, ntx), corner(img, h, w, xa1, yb1, ntx), wa, nb);
-        }
+    float* __restrict__ outp = P.out + ((int64_t)b * P.C + (int64_t)lv * WS::KK) * P.q_count + q0 + g;
+    for (int k = part; k < WS::KK; k += 4) {
+        const float res = sample_level<R, QB>(st, P, lv, b, q0, g, k, md);
         // non-temporal: the 324-channel output is consumed by the next kernel, not re-read here;
         // keeping it out of the caches leaves the Infinity Cache to the pyramid windows, which the
         // next lookup re-reads (tools/lookup_lab.hip: -11% lookup time)

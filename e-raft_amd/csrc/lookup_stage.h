@@ -1,0 +1,155 @@
+// lookup_stage.h -- the per-level window staging shared by the lookup kernel (lookup.hip) and the
+// fused lookup + convc1 kernel (motion.hip).  Device code only, gfx950.
+//
+// For a group of QB consecutive queries of one batch item and one pyramid level (NTQ threads,
+// NTQ / QB threads per query):
+//   stage_level()   phase 0: the 2(2r+1) coordinate chains per query -- x chains depend on the
+//                   x-offset a only, y chains on the y-offset b only (corr.py:41-43), each the
+//                   reference's exact fp32 sequence (utils.py:11-12 + ATen's unnormalize) -> floor
+//                   and fraction into LDS;
+//                   phase 1: each query's (2r+3)^2 window (one slack row/column absorbs the +-1
+//                   floor flips of the normalize/unnormalize round trip) staged into LDS with raw
+//                   buffer loads whose range check implements grid_sample's zero padding;
+//   sample_level()  phase 2: output channel k = a(2r+1) + b of query g, blended from LDS in
+//                   ATen's order; coordinates that do not fit the window (NaN/inf/huge) take an
+//                   exact direct-gather path.
+#pragma once
+#include "ecorr_device.h"
+#include "ecorr_internal.h"
+
+namespace ecorr {
+
+template <int R, int QB>
+struct WindowStage {
+    static constexpr int K = 2 * R + 1;   // samples per axis
+    static constexpr int KK = K * K;
+    static constexpr int S = 2 * R + 3;   // staged window side
+    static constexpr int SS = S * S;
+    static constexpr int SP = SS | 1;     // odd per-query stride: conflict-free lanes = queries
+    float win[QB * SP];
+    float fx[QB][K], wx[QB][K], fy[QB][K], wy[QB][K];
+    // per query: window origin x, y and (mode | needed cols << 8 | needed rows << 16), where mode
+    // 0 = staged, 1 = direct gather (coordinates that do not fit the window), 2 = past the range.
+    int org[QB][3];
+};
+
+// Phases 0 and 1 for level lv of queries [q0, q0 + QB) of batch item b; ends with a barrier.
+template <int R, int QB, int NTQ>
+__device__ __forceinline__ void stage_level(WindowStage<R, QB>& st, const LookupParams& P, int lv, int b, int q0,
+                                            int tid) {
+    using WS = WindowStage<R, QB>;
+    constexpr int K = WS::K, S = WS::S, SP = WS::SP;
+    constexpr int TPQ = NTQ / QB;   // threads per query
+    const int g = tid % QB, part = tid / QB;
+    const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
+    const int p = q0 + g;
+    const bool valid = p < P.q_count;
+    const int64_t Q = P.q_count;   // coords slab stride
+    const int64_t hw = P.lsz[lv];  // floats per query image
+    const float* __restrict__ lvbase = P.lvl[lv] + ((int64_t)b * P.q_count + q0) * hw;
+
+    // ---- phase 0: coordinate chains (corr.py:41-43, utils.py:11-12, grid_sampler unnormalize)
+    if (valid) {
+        const float inv = 1.0f / (float)(1 << lv);  // coords / 2**i is an exact scaling
+        const float cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
+        const float cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);
+        const float wm1 = (float)(w - 1), hm1 = (float)(h - 1);
+#pragma unroll
+        for (int j = part; j < 2 * K; j += TPQ) {
+            const bool isx = j < K;
+            const int o = isx ? j : j - K;
+            const float c = __fadd_rn(isx ? cx : cy, (float)(o - R));
+            const float m1 = isx ? wm1 : hm1;
+            const float v = unnormalize(c, m1, m1 * 0.5f);
+            const float f = floorf(v);
+            if (isx) { st.fx[g][o] = f; st.wx[g][o] = __fsub_rn(v, f); }
+            else     { st.fy[g][o] = f; st.wy[g][o] = __fsub_rn(v, f); }
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 0b: window origin and fast/slow decision per query
+    if (part == 0) {
+        int md = 2, X0 = 0, Y0 = 0, NX = 0, NY = 0;
+        if (valid) {
+            const float x0 = st.fx[g][0], y0 = st.fy[g][0];
+            bool ok = fabsf(x0) < 1.0e7f && fabsf(y0) < 1.0e7f;  // false for NaN / inf / huge
+#pragma unroll
+            for (int o = 0; o < K; ++o) {
+                const float dx = st.fx[g][o] - x0, dy = st.fy[g][o] - y0;  // exact: integers < 2^24
+                ok &= (dx >= 0.0f) & (dx <= (float)(S - 2)) & (dy >= 0.0f) & (dy <= (float)(S - 2));
+            }
+            md = ok ? 0 : 1;
+            X0 = ok ? (int)x0 : 0;
+            Y0 = ok ? (int)y0 : 0;
+            // corners span [x0, floor(ix_last) + 1]: monotone round trip, so the last sample bounds it
+            NX = ok ? (int)(st.fx[g][K - 1] - x0) + 2 : 0;
+            NY = ok ? (int)(st.fy[g][K - 1] - y0) + 2 : 0;
+        }
+        st.org[g][0] = X0;
+        st.org[g][1] = Y0;
+        st.org[g][2] = md | (NX << 8) | (NY << 16);
+    }
+    __syncthreads();
+
+    // ---- phase 1: stage windows, zeros outside the image (grid_sample padding_mode='zeros').
+    // Work item = (query, window column); each item walks the S rows.  Loads are raw buffer loads
+    // over this group's slab of the level: an element outside the image gets an out-of-range
+    // offset and the hardware range check returns 0 -- zero padding with no branch and no select,
+    // so all NCOL*S loads of a thread issue back to back.
+    constexpr int ITEMS = QB * S;
+    constexpr int NCOL = (ITEMS + NTQ - 1) / NTQ;
+    const int nq = min(QB, P.q_count - q0);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lvbase), 0, (int)(nq * hw * 4), 0x00020000);
+    constexpr int OOB = 0x7ffffff0;   // beyond any slab: reads as 0
+    float vals[NCOL][S];
+    int dst[NCOL];
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) {
+        const int it = tid + c * NTQ;
+        const bool live = it < ITEMS;
+        const int gq = live ? it / S : 0;
+        const int rx = it - gq * S;
+        const int x = st.org[gq][0] + rx, y0 = st.org[gq][1], info = st.org[gq][2];
+        const int ny = (info >> 16) & 0xff;
+        // only the needed corner rectangle touches memory; the slack row/column reads 0 for free
+        const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) && (unsigned)x < (unsigned)w;
+        const int base = (int)(gq * hw);
+        dst[c] = live ? gq * SP + rx : -1;
+#pragma unroll
+        for (int ry = 0; ry < S; ++ry) {
+            const int y = y0 + ry;
+            const int off = (colin && ry < ny && (unsigned)y < (unsigned)h) ? (base + level_off(y, x, ntx, w)) * 4 : OOB;
+            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c)
+        if (dst[c] >= 0)
+#pragma unroll
+            for (int ry = 0; ry < S; ++ry) st.win[dst[c] + ry * S] = vals[c][ry];
+    __syncthreads();
+}
+
+// Phase 2: sample k = a(2r+1) + b of query g (staged mode md = 0 or direct mode md = 1).
+template <int R, int QB>
+__device__ __forceinline__ float sample_level(const WindowStage<R, QB>& st, const LookupParams& P, int lv, int b,
+                                              int q0, int g, int k, int md) {
+    using WS = WindowStage<R, QB>;
+    constexpr int K = WS::K, S = WS::S, SP = WS::SP;
+    const int a = k / K, bb = k - a * K;
+    const float xa = st.fx[g][a], yb = st.fy[g][bb];
+    const float wa = st.wx[g][a], nb = st.wy[g][bb];
+    if (md == 0) {
+        const float* c = st.win + g * SP + ((int)yb - st.org[g][1]) * S + ((int)xa - st.org[g][0]);
+        return blend(c[0], c[1], c[S], c[S + 1], wa, nb);
+    }
+    const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
+    const float* img = P.lvl[lv] + ((int64_t)b * P.q_count + q0 + g) * (int64_t)P.lsz[lv];
+    const float xa1 = __fadd_rn(xa, 1.0f), yb1 = __fadd_rn(yb, 1.0f);
+    return blend(corner(img, h, w, xa, yb, ntx), corner(img, h, w, xa1, yb, ntx),
+                 corner(img, h, w, xa, yb1, ntx), corner(img, h, w, xa1, yb1, ntx), wa, nb);
+}
+
+}  // namespace ecorr

@@ -100,8 +100,9 @@ class BasicMotionEncoder(nn.Module):
         self.convf2 = nn.Conv2d(128, 64, 3, padding=1)
         self.conv = nn.Conv2d(64 + 192, 128 - 2, 3, padding=1)
 
-    def forward(self, flow, corr):
-        c = F.relu(self.convc2(F.relu(self.convc1(corr))))
+    def forward(self, flow, corr, corr_is_convc1=False):
+        # corr_is_convc1: `corr` already is F.relu(convc1(corr)) -- the fused CorrBlock path
+        c = F.relu(self.convc2(corr if corr_is_convc1 else F.relu(self.convc1(corr))))
         f = F.relu(self.convf2(F.relu(self.convf1(flow))))
         out = F.relu(self.conv(torch.cat([c, f], dim=1)))
         return torch.cat([out, flow], dim=1)
@@ -150,8 +151,8 @@ class BasicUpdateBlock(nn.Module):
         self.mask = nn.Sequential(nn.Conv2d(128, 256, 3, padding=1), nn.ReLU(inplace=True),
                                   nn.Conv2d(256, 64 * 9, 1, padding=0))
 
-    def forward(self, net, inp, corr, flow):
-        inp = torch.cat([inp, self.encoder(flow, corr)], dim=1)
+    def forward(self, net, inp, corr, flow, corr_is_convc1=False):
+        inp = torch.cat([inp, self.encoder(flow, corr, corr_is_convc1)], dim=1)
         net = self.gru(net, inp)
         return net, 0.25 * self.mask(net), self.flow_head(net)
 
@@ -180,13 +181,17 @@ class ImagePadder:
 
 class ERAFT(nn.Module):
     """E-RAFT with the MI355X CorrBlock (eraft.py:37-145).  config needs 'subtype' in
-    {'standard', 'warm_start'}; n_first_channels = voxel bins."""
+    {'standard', 'warm_start'}; n_first_channels = voxel bins.  fuse_motion_corr=True replaces
+    `corr_fn(coords1)` + BasicMotionEncoder's `relu(convc1(corr))` with the fused HIP kernel
+    (CorrBlock.lookup_conv1x1_relu); the default keeps the reference's call
+    pattern exactly."""
 
     corr_levels = 4
     corr_radius = 4
 
-    def __init__(self, config, n_first_channels):
+    def __init__(self, config, n_first_channels, fuse_motion_corr=False):
         super().__init__()
+        self.fuse_motion_corr = fuse_motion_corr
         self.image_padder = ImagePadder(min_size=32)
         self.subtype = config["subtype"].lower()
         if self.subtype not in ("standard", "warm_start"):
@@ -228,8 +233,13 @@ class ERAFT(nn.Module):
         predictions = []
         for _ in range(iters):
             coords1 = coords1.detach()
-            corr = corr_fn(coords1)
-            net, up_mask, delta = self.update_block(net, inp, corr, coords1 - coords0)
+            if self.fuse_motion_corr:
+                c1 = self.update_block.encoder.convc1
+                corr = corr_fn.lookup_conv1x1_relu(coords1, c1.weight, c1.bias)
+            else:
+                corr = corr_fn(coords1)
+            net, up_mask, delta = self.update_block(net, inp, corr, coords1 - coords0,
+                                                    corr_is_convc1=self.fuse_motion_corr)
             coords1 = coords1 + delta
             predictions.append(self.image_padder.unpad(self.upsample_flow(coords1 - coords0, up_mask)))
         return coords1 - coords0, predictions

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 4
+#define ECORR_ABI_VERSION 5
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -71,6 +71,16 @@ int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int
  * Replaces: CorrBlock.__call__ (corr.py:29-50) incl. bilinear_sampler (utils.py:7-21). */
 int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
                  int levels, int radius, float* out, void* stream);
+
+/* Lookup fused with its consumer, BasicMotionEncoder's convc1 + ReLU:
+ * out float[B][O][q_count] = relu(bias[o] + sum_c weight[o][c] * corr[b][c][p]), where corr is
+ * exactly what ecorr_lookup would return (C = levels*(2r+1)^2 channels) and never leaves the chip.
+ * weight: float[O][C] (the conv weight [O][C][1][1] as stored), bias: float[O] or NULL.
+ * radius must be 4 and levels <= 4 (else ECORR_ERADIUS), O a positive multiple of 64.
+ * Replaces: CorrBlock.__call__ (corr.py:29-50) + F.relu(self.convc1(corr)) (update.py:67,74). */
+int ecorr_lookup_conv1x1_relu(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
+                              int levels, int radius, const float* weight, const float* bias, int O,
+                              float* out, void* stream);
 
 /* Generic bilinear_sampler: img float[N][C][h][w], coords float[N][Hg][Wg][2] in pixels ->
  * out float[N][C][Hg][Wg]; mask (nullable) float[N][Hg][Wg] = 1 where the normalized sample

@@ -87,6 +87,12 @@ def test_argument_validation_before_launch(ea):
     assert L.ecorr_lookup(8, 8, 1, 8, 8, 64, 0, 4, 8, None) == _lib.ECORR_ELEVELS
     assert L.ecorr_lookup(8, 8, 1, 4, 4, 16, 4, 4, 8, None) == _lib.ECORR_ESHAPE
     assert "too small" in _lib.strerror(_lib.ECORR_ESHAPE)
+    # fused lookup + convc1: radius 4 / <= 4 levels only, O a multiple of 64, weight required
+    F = L.ecorr_lookup_conv1x1_relu
+    assert F(8, 8, 1, 16, 16, 256, 4, 3, 8, None, 64, 8, None) == _lib.ECORR_ERADIUS
+    assert F(8, 8, 1, 64, 64, 4096, 5, 4, 8, None, 64, 8, None) == _lib.ECORR_ERADIUS
+    assert F(8, 8, 1, 16, 16, 256, 4, 4, 8, None, 96, 8, None) == _lib.ECORR_EINVAL
+    assert F(8, 8, 1, 16, 16, 256, 4, 4, None, None, 64, 8, None) == _lib.ECORR_EINVAL
 
 
 def test_cpu_tensors_rejected_loudly(ea):

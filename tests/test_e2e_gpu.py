@@ -34,14 +34,14 @@ def epe(a, b):
     return float(np.mean(np.sqrt(np.sum(d * d, axis=1))))
 
 
-def _run(z, corr_cls=None):
+def _run(z, corr_cls=None, fuse=False):
     import eraft_amd.network as nw
     H, W, bins, seed = int(z["H"]), int(z["W"]), int(z["bins"]), int(z["seed"])
     saved = nw.CorrBlock
     if corr_cls is not None:
         nw.CorrBlock = corr_cls
     try:
-        net = nw.ERAFT({"subtype": str(z["subtype"])}, n_first_channels=bins)
+        net = nw.ERAFT({"subtype": str(z["subtype"])}, n_first_channels=bins, fuse_motion_corr=fuse)
         net.load_state_dict(make_state_dict(net.state_dict()))
         net = net.eval().cuda()
         im1 = torch.from_numpy(prng.normal(seed, (1, bins, H, W))).cuda()
@@ -77,3 +77,20 @@ def test_e2e_flow_matches_reference(path):
     assert e_up <= EPE_TOL
     assert c_up <= EPE_TOL / 10
 
+
+
+@pytest.mark.parametrize("path", CASES, ids=lambda p: os.path.basename(p)[:-4])
+def test_e2e_fused_motion_corr(path):
+    """Same bar with the fused lookup + convc1 + ReLU kernel."""
+    if not torch.cuda.is_available():
+        pytest.fail("no HIP device visible")
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    z = np.load(path)
+    low, (_, up) = _run(z, fuse=True)
+    base_low, (_, base_up) = _run(z)
+    e_low, e_up = epe(low, z["flow_low"]), epe(up, z["flow_up"])
+    print(f"{os.path.basename(path)} fused: EPE vs reference low {e_low:.3g} px, up {e_up:.3g} px | "
+          f"vs unfused (same GPU) low {epe(low, base_low):.3g} up {epe(up, base_up):.3g}")
+    assert e_low <= EPE_TOL
+    assert e_up <= EPE_TOL

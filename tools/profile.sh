@@ -3,8 +3,8 @@
 # (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass).  Usage: tools/profile.sh TAG [bench args]
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-prof}; shift
-ARGS=${@:---steps 3 --warmup 1 --no-cpu-baseline}
-KT_ARGS=${KT_ARGS:---steps 20 --warmup 5 --no-cpu-baseline}
+ARGS=${@:---steps 3 --warmup 1 --no-cpu-baseline --no-next}
+KT_ARGS=${KT_ARGS:---steps 20 --warmup 5 --no-cpu-baseline --no-next}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
