@@ -151,6 +151,43 @@ def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
             "work_per_launch": f"{flops:.4g} flop (1x1 conv 324->256 over B*H*W queries)"}
 
 
+def measure_forward_interpolate(B, H, W, device, reps=5):
+    """the warm-start splat (utils/image_utils.py:50-83) over the batch's
+    [B, 2, H, W] low-res flow -- our one launch (splat.hip) against the reference's op sequence
+    (oracle/torch_ref.py: per-sample loop of ATen put_ scatters) on this GPU and on the host CPU.
+    Latency-bound: 16 B of algorithmic traffic per pixel (flow in, flow out)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch_ref
+    import eraft_amd
+    g = torch.Generator(device=device).manual_seed(5)
+    flow = torch.nn.functional.avg_pool2d(torch.randn((B, 2, H, W), generator=g, device=device) * 9.0,
+                                          5, stride=1, padding=2).contiguous()
+    stream = torch.cuda.current_stream(device)
+
+    def gpu_ms(fn):
+        ts = []
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return sorted(ts[1:])[len(ts[1:]) // 2]
+
+    ours = gpu_ms(lambda: eraft_amd.forward_interpolate_pytorch(flow))
+    ref_gpu = gpu_ms(lambda: torch_ref.forward_interpolate_pytorch(flow))
+    fc = flow.cpu()
+    t0 = time.perf_counter()
+    torch_ref.forward_interpolate_pytorch(fc)
+    ref_cpu = (time.perf_counter() - t0) * 1e3
+    return {"ms_per_call": round(ours, 4), "batch": B, "flow": [2, H, W],
+            "reference_ops_on_gpu_ms": round(ref_gpu, 3), "reference_ops_on_cpu_ms": round(ref_cpu, 3),
+            "speedup_vs_reference_gpu": round(ref_gpu / ours, 1), "bound": "latency",
+            "achieved_GBs": round(16.0 * B * H * W / (ours * 1e-3) / 1e9, 2),
+            "note": "bit-exact with the reference's serial CPU put_; one launch for the whole batch"}
+
+
 def pmc_traffic(kernel_prefix):
     """HBM bytes per dispatch of the dominant kernel from the committed PMC summary of this same
     bench command (profiles/latest_pmc.json, written by tools/pmc_summary.py), else None."""
@@ -284,7 +321,8 @@ def main():
     }
     if a.mode == "batch" and world == 1 and not a.no_next:
         with torch.no_grad():
-            res["next_rows"] = {"lookup_conv1x1_relu": measure_fused_convc1(make_block(), coords, B, H, W, device)}
+            res["next_rows"] = {"lookup_conv1x1_relu": measure_fused_convc1(make_block(), coords, B, H, W, device),
+                                "forward_interpolate": measure_forward_interpolate(B, H, W, device)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(B, D, H, W, iters, a.cpu_seconds)
     if rank == 0:

@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -45,6 +45,12 @@ SYMBOLS = {
     "ecorr_pyramid_tile": (_i, [ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     # (H, W, levels, ntx[levels])
     "ecorr_pyramid_formats": (_i, [_i, _i, _i, ctypes.POINTER(_i)]),
+    # (B, n, h, w, bytes*)
+    "ecorr_splat_workspace_size": (_i, [_i, _i64, _i, _i, ctypes.POINTER(_i64)]),
+    # (flow, B, h, w, out, workspace, stream)
+    "ecorr_forward_interpolate": (_i, [_p, _i, _i, _i, _p, _p, _p]),
+    # (pts, n, h, w, values, valid, workspace, stream)
+    "ecorr_grid_sample_values": (_i, [_p, _i64, _i, _i, _p, _p, _p, _p]),
 }
 
 

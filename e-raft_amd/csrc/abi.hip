@@ -182,3 +182,32 @@ ECORR_EXPORT int ecorr_coords_grid(int B, int H, int W, float* out, void* stream
     if (!out || B <= 0 || H <= 0 || W <= 0) return ECORR_EINVAL;
     return launch_coords_grid(B, H, W, out, (hipStream_t)stream);
 }
+
+namespace {
+
+bool splat_dims_ok(int B, int64_t n, int h, int w) {
+    return B > 0 && n >= 0 && n < (1 << 24) && h > 0 && w > 0 && (int64_t)h * w <= 0x7fffffff;
+}
+
+}  // namespace
+
+ECORR_EXPORT int ecorr_splat_workspace_size(int B, int64_t n, int h, int w, int64_t* bytes) {
+    if (!bytes || !splat_dims_ok(B, n, h, w)) return ECORR_EINVAL;
+    *bytes = splat_workspace_bytes(false, B, n, h, w);   // points mode is the stricter LDS fit
+    return ECORR_OK;
+}
+
+ECORR_EXPORT int ecorr_forward_interpolate(const float* flow, int B, int h, int w, float* out, void* workspace,
+                                           void* stream) {
+    const int64_t n = (int64_t)h * w;
+    if (!flow || !out || !splat_dims_ok(B, n, h, w)) return ECORR_EINVAL;
+    if (!workspace && splat_workspace_bytes(true, B, n, h, w) > 0) return ECORR_EINVAL;
+    return launch_splat(true, flow, B, n, h, w, out, nullptr, workspace, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_grid_sample_values(const float* pts, int64_t n, int h, int w, float* values, uint8_t* valid,
+                                          void* workspace, void* stream) {
+    if (!values || (!pts && n > 0) || !splat_dims_ok(1, n, h, w)) return ECORR_EINVAL;
+    if (!workspace && splat_workspace_bytes(false, 1, n, h, w) > 0) return ECORR_EINVAL;
+    return launch_splat(false, pts, 1, n, h, w, values, valid, workspace, (hipStream_t)stream);
+}

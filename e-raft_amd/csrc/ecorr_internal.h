@@ -63,4 +63,8 @@ int launch_bilinear_sampler(const float* img, int N, int C, int h, int w, const 
 
 int launch_coords_grid(int B, int H, int W, float* out, hipStream_t stream);
 
+int64_t splat_workspace_bytes(bool flow_mode, int B, int64_t n, int h, int w);
+int launch_splat(bool flow_mode, const float* pts, int B, int64_t n, int h, int w, float* values, uint8_t* valid,
+                 void* workspace, hipStream_t stream);
+
 }  // namespace ecorr

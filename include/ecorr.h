@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 5
+#define ECORR_ABI_VERSION 6
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -91,6 +91,26 @@ int ecorr_bilinear_sampler(const float* img, int N, int C, int h, int w, const f
 /* coords_grid: out float[B][2][H][W], channel 0 = x (column), 1 = y (row).
  * Replaces: model/utils.py:24-27. */
 int ecorr_coords_grid(int B, int H, int W, float* out, void* stream);
+
+/* ---- the warm-start splat (utils/image_utils.py) ----
+ * Deterministic and bit-exact with the reference's serial CPU put_(accumulate=True): the scatter
+ * runs as a counting sort + ordered gather in a caller-provided workspace. */
+
+/* Workspace bytes for B items of n points splatted onto an h x w grid (B = 1 for
+ * ecorr_grid_sample_values, n = h*w for ecorr_forward_interpolate). */
+int ecorr_splat_workspace_size(int B, int64_t n, int h, int w, int64_t* bytes);
+
+/* forward_interpolate_pytorch: flow float[B][2][h][w] -> out float[B][2][h][w]; every pixel moves
+ * to (col + dx, row + dy) and is splatted bilinearly; pixels nothing lands on read 0.
+ * Replaces: utils/image_utils.py:50-83 (and its per-sample Python loop, :78-80). */
+int ecorr_forward_interpolate(const float* flow, int B, int h, int w, float* out, void* workspace,
+                              void* stream);
+
+/* grid_sample_values: pts float[3][n] rows x, y, z -> values float[h][w] (interpolated z) and
+ * valid uint8[h][w] (nullable; 1 where some weight landed).  0 <= n < 2^24.
+ * Replaces: utils/image_utils.py:10-47. */
+int ecorr_grid_sample_values(const float* pts, int64_t n, int h, int w, float* values, uint8_t* valid,
+                             void* workspace, void* stream);
 
 /* Tile shape of the pyramid storage (ECORR_TILE_H, ECORR_TILE_W). */
 int ecorr_pyramid_tile(int* tile_h, int* tile_w);

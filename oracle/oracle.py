@@ -37,6 +37,11 @@ def lib():
         L.oracle_bilinear_sampler.argtypes = [_f32p] + [ctypes.c_int] * 4 + [
             _f32p, ctypes.c_int, ctypes.c_int, _f32p, ctypes.c_void_p]
         L.oracle_coords_grid.argtypes = [ctypes.c_int] * 3 + [_f32p]
+        L.oracle_grid_sample_values.argtypes = [_f32p, _f32p, ctypes.c_void_p, ctypes.c_int, ctypes.c_long,
+                                                 ctypes.c_int, ctypes.c_int, _f32p, ctypes.c_void_p]
+        L.oracle_forward_interpolate.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p]
+        for fn in ("oracle_grid_sample_values", "oracle_forward_interpolate"):
+            getattr(L, fn).restype = None
         for fn in ("oracle_corr_level0", "oracle_avg_pool2", "oracle_lookup",
                    "oracle_bilinear_sampler", "oracle_coords_grid"):
             getattr(L, fn).restype = None
@@ -132,3 +137,28 @@ def same_bits(a, b):
     if not np.array_equal(na, nb):
         return False
     return bool(np.array_equal(a.view(np.uint32)[~na], b.view(np.uint32)[~nb]))
+
+
+# ---- SURVEY §8f rows (next_oracle.c) ----
+
+def forward_interpolate(flow):
+    """image_utils.py:50-83: flow [B,2,h,w] (or [2,h,w]) -> [B,2,h,w]."""
+    flow = _c(flow)
+    if flow.ndim == 3:
+        flow = flow[None]
+    B, _, h, w = flow.shape
+    out = np.empty_like(flow)
+    lib().oracle_forward_interpolate(flow, B, h, w, out)
+    return out
+
+
+def grid_sample_values(inp, h, w):
+    """image_utils.py:10-47: inp [3, n] -> (values [1,h,w] f32, valid [1,h,w] bool)."""
+    inp = _c(inp).reshape(3, -1)
+    n = inp.shape[1]
+    values = np.empty((1, h, w), dtype=np.float32)
+    valid = np.empty((1, h, w), dtype=np.uint8)
+    z = inp[2].copy()
+    lib().oracle_grid_sample_values(inp[0].copy(), inp[1].copy(), z.ctypes.data, 1, n, h, w, values,
+                                    valid.ctypes.data)
+    return values, valid.astype(bool)

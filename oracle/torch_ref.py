@@ -44,3 +44,47 @@ class TorchCpuCorrBlock:
             s = F.grid_sample(img, grid, align_corners=True)
             outs.append(s.view(B, H, W, -1))
         return torch.cat(outs, dim=-1).permute(0, 3, 1, 2).contiguous().float()
+
+
+def grid_sample_values(input, height, width):
+    """utils/image_utils.py:10-47, same ATen ops in the same order (ceil/floor, put_ accumulate)."""
+    device = input.device
+    ceil = torch.stack([torch.ceil(input[0, :]), torch.ceil(input[1, :]), input[2, :]])
+    floor = torch.stack([torch.floor(input[0, :]), torch.floor(input[1, :]), input[2, :]])
+    z = input[2, :].clone()
+    values_ipl = torch.zeros(height * width, device=device)
+    weights_acc = torch.zeros(height * width, device=device)
+    for x_vals in [floor[0], ceil[0]]:
+        for y_vals in [floor[1], ceil[1]]:
+            m = (x_vals < width) & (x_vals >= 0) & (y_vals < height) & (y_vals >= 0)
+            weights = (1 - (input[0] - x_vals).abs()) * (1 - (input[1] - y_vals).abs())
+            idx = (x_vals + width * y_vals).long()
+            values_ipl.put_(idx[m], (z * weights)[m], accumulate=True)
+            weights_acc.put_(idx[m], weights[m], accumulate=True)
+    valid = weights_acc.clone()
+    valid[valid > 0] = 1
+    valid = valid.bool().reshape([height, width])
+    values = (values_ipl / (weights_acc + 1e-15)).reshape([height, width])
+    return values.unsqueeze(0).clone(), valid.unsqueeze(0).clone()
+
+
+def forward_interpolate_pytorch(flow_in):
+    """utils/image_utils.py:50-83 (per-sample loop over the batch, as in the reference)."""
+    flow = flow_in.clone()
+    if len(flow.shape) < 4:
+        flow = flow.unsqueeze(0)
+    b, _, h, w = flow.shape
+    device = flow.device
+    dx, dy = flow[:, 0], flow[:, 1]
+    y0, x0 = torch.meshgrid(torch.arange(0, h, 1), torch.arange(0, w, 1), indexing="ij")
+    x0 = torch.stack([x0] * b).to(device)
+    y0 = torch.stack([y0] * b).to(device)
+    x1 = (x0 + dx).flatten(start_dim=1)
+    y1 = (y0 + dy).flatten(start_dim=1)
+    dx = dx.flatten(start_dim=1)
+    dy = dy.flatten(start_dim=1)
+    flow_new = torch.zeros(flow.shape, device=device)
+    for i in range(b):
+        flow_new[i, 0] = grid_sample_values(torch.stack([x1[i], y1[i], dx[i]]), h, w)[0]
+        flow_new[i, 1] = grid_sample_values(torch.stack([x1[i], y1[i], dy[i]]), h, w)[0]
+    return flow_new

@@ -26,3 +26,11 @@ def test_torch_ref_matches_reference(path):
         if k.startswith("coords_"):
             s = k[len("coords_"):]
             assert oracle.same_bits(blk(torch.from_numpy(z[k])).numpy(), z[f"out_{s}"]), s
+
+
+def test_torch_ref_splat_matches_reference():
+    import torch_ref
+    z = np.load(os.path.join(GOLDEN, "next_splat.npz"))
+    for k in sorted(f.split("/")[0] for f in z.files if f.startswith("fi_") and f.endswith("/flow")):
+        got = torch_ref.forward_interpolate_pytorch(torch.from_numpy(z[f"{k}/flow"])).numpy()
+        assert oracle.same_bits(got, z[f"{k}/out"]), k
