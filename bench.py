@@ -188,6 +188,44 @@ def measure_forward_interpolate(B, H, W, device, reps=5):
             "note": "bit-exact with the reference's serial CPU put_; one launch for the whole batch"}
 
 
+def measure_upsample(B, H, W, device, reps=5):
+    """convex 8x upsampling (eraft.py:74-85) of a [B, 2, H, W] flow with its
+    [B, 576, H, W] mask -- one HIP pass (upsample.hip) vs the reference's ATen expression on this
+    GPU; HBM-bound: 2304 B of mask + 8 B of flow in, 512 B out per low-res pixel."""
+    import eraft_amd
+    import torch.nn.functional as F
+    g = torch.Generator(device=device).manual_seed(6)
+    flow = torch.randn((B, 2, H, W), generator=g, device=device) * 3.0
+    mask = torch.randn((B, 576, H, W), generator=g, device=device) * 0.25
+    stream = torch.cuda.current_stream(device)
+
+    def ref():
+        m = torch.softmax(mask.view(B, 1, 9, 8, 8, H, W), dim=2)
+        up = F.unfold(8 * flow, [3, 3], padding=1).view(B, 2, 9, 1, 1, H, W)
+        return torch.sum(m * up, dim=2).permute(0, 1, 4, 2, 5, 3).reshape(B, 2, 8 * H, 8 * W)
+
+    def gpu_ms(fn, n=10):
+        ts = []
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(n):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / n)
+        return sorted(ts[1:])[len(ts[1:]) // 2]
+
+    ours = gpu_ms(lambda: eraft_amd.upsample_flow(flow, mask))
+    theirs = gpu_ms(ref)
+    nbytes = B * H * W * (576 * 4 + 2 * 4 + 2 * 64 * 4)
+    gbs = nbytes / (ours * 1e-3) / 1e9
+    return {"ms_per_call": round(ours, 4), "reference_expr_on_gpu_ms": round(theirs, 4),
+            "speedup": round(theirs / ours, 2), "bound": "hbm", "achieved": round(gbs, 1),
+            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "work_per_launch": f"{nbytes:.4g} B (mask + flow in, 8x flow out)"}
+
+
 def pmc_traffic(kernel_prefix):
     """HBM bytes per dispatch of the dominant kernel from the committed PMC summary of this same
     bench command (profiles/latest_pmc.json, written by tools/pmc_summary.py), else None."""
@@ -322,7 +360,8 @@ def main():
     if a.mode == "batch" and world == 1 and not a.no_next:
         with torch.no_grad():
             res["next_rows"] = {"lookup_conv1x1_relu": measure_fused_convc1(make_block(), coords, B, H, W, device),
-                                "forward_interpolate": measure_forward_interpolate(B, H, W, device)}
+                                "forward_interpolate": measure_forward_interpolate(B, H, W, device),
+                                "upsample_flow": measure_upsample(B, H, W, device)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(B, D, H, W, iters, a.cpu_seconds)
     if rank == 0:

@@ -10,6 +10,8 @@ importable as `eraft_amd`.  Kernels: e-raft_amd/csrc (HIP, C ABI include/ecorr.h
 from .corr import CorrBlock
 from .utils import bilinear_sampler, coords_grid
 from .image_utils import forward_interpolate_pytorch, grid_sample_values
+from .flow import flow_16bit_to_float, flow_to_png16, upsample_flow
 from ._lib import LIB_PATH, lib
 
-__all__ = ["CorrBlock", "bilinear_sampler", "coords_grid", "forward_interpolate_pytorch", "grid_sample_values", "LIB_PATH", "lib"]
+__all__ = ["CorrBlock", "bilinear_sampler", "coords_grid", "forward_interpolate_pytorch", "grid_sample_values",
+           "upsample_flow", "flow_to_png16", "flow_16bit_to_float", "LIB_PATH", "lib"]

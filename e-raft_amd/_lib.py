@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -51,6 +51,12 @@ SYMBOLS = {
     "ecorr_forward_interpolate": (_i, [_p, _i, _i, _i, _p, _p, _p]),
     # (pts, n, h, w, values, valid, workspace, stream)
     "ecorr_grid_sample_values": (_i, [_p, _i64, _i, _i, _p, _p, _p, _p]),
+    # (flow, mask, N, H, W, out, stream)
+    "ecorr_upsample_flow": (_i, [_p, _p, _i, _i, _i, _p, _p]),
+    # (flow, B, h, w, out_u16, stream)
+    "ecorr_flow_to_png16": (_i, [_p, _i, _i, _i, _p, _p]),
+    # (in_u16, B, h, w, flow, valid, bad, stream)
+    "ecorr_png16_to_flow": (_i, [_p, _i, _i, _i, _p, _p, _p, _p]),
 }
 
 

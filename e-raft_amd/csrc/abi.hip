@@ -211,3 +211,21 @@ ECORR_EXPORT int ecorr_grid_sample_values(const float* pts, int64_t n, int h, in
     if (!workspace && splat_workspace_bytes(false, 1, n, h, w) > 0) return ECORR_EINVAL;
     return launch_splat(false, pts, 1, n, h, w, values, valid, workspace, (hipStream_t)stream);
 }
+
+ECORR_EXPORT int ecorr_upsample_flow(const float* flow, const float* mask, int N, int H, int W, float* out,
+                                     void* stream) {
+    if (!flow || !mask || !out || N <= 0 || N > 65535 || H <= 0 || W <= 0 || (int64_t)H * W > (1 << 26))
+        return ECORR_EINVAL;
+    return launch_upsample_flow(flow, mask, N, H, W, out, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_flow_to_png16(const float* flow, int B, int h, int w, uint16_t* out, void* stream) {
+    if (!flow || !out || B <= 0 || h <= 0 || w <= 0) return ECORR_EINVAL;
+    return launch_png16_encode(flow, B, h, w, out, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_png16_to_flow(const uint16_t* in, int B, int h, int w, float* flow, uint8_t* valid, int* bad,
+                                     void* stream) {
+    if (!in || !flow || !valid || !bad || B <= 0 || h <= 0 || w <= 0) return ECORR_EINVAL;
+    return launch_png16_decode(in, B, h, w, flow, valid, bad, (hipStream_t)stream);
+}

@@ -63,6 +63,11 @@ int launch_bilinear_sampler(const float* img, int N, int C, int h, int w, const 
 
 int launch_coords_grid(int B, int H, int W, float* out, hipStream_t stream);
 
+int launch_upsample_flow(const float* flow, const float* mask, int N, int H, int W, float* out, hipStream_t stream);
+int launch_png16_encode(const float* flow, int B, int h, int w, uint16_t* out, hipStream_t stream);
+int launch_png16_decode(const uint16_t* in, int B, int h, int w, float* flow, uint8_t* valid, int* bad,
+                        hipStream_t stream);
+
 int64_t splat_workspace_bytes(bool flow_mode, int B, int64_t n, int h, int w);
 int launch_splat(bool flow_mode, const float* pts, int B, int64_t n, int h, int w, float* values, uint8_t* valid,
                  void* workspace, hipStream_t stream);

@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .corr import CorrBlock
+from .flow import upsample_flow as hip_upsample_flow
 from .utils import coords_grid
 
 
@@ -183,15 +184,17 @@ class ERAFT(nn.Module):
     """E-RAFT with the MI355X CorrBlock (eraft.py:37-145).  config needs 'subtype' in
     {'standard', 'warm_start'}; n_first_channels = voxel bins.  fuse_motion_corr=True replaces
     `corr_fn(coords1)` + BasicMotionEncoder's `relu(convc1(corr))` with the fused HIP kernel
-    (CorrBlock.lookup_conv1x1_relu); the default keeps the reference's call
-    pattern exactly."""
+    (CorrBlock.lookup_conv1x1_relu); hip_upsample=True runs upsample_flow as
+    the one-pass HIP kernel (eraft_amd.upsample_flow).  The defaults keep the
+    reference's call pattern exactly."""
 
     corr_levels = 4
     corr_radius = 4
 
-    def __init__(self, config, n_first_channels, fuse_motion_corr=False):
+    def __init__(self, config, n_first_channels, fuse_motion_corr=False, hip_upsample=False):
         super().__init__()
         self.fuse_motion_corr = fuse_motion_corr
+        self.hip_upsample = hip_upsample
         self.image_padder = ImagePadder(min_size=32)
         self.subtype = config["subtype"].lower()
         if self.subtype not in ("standard", "warm_start"):
@@ -241,5 +244,6 @@ class ERAFT(nn.Module):
             net, up_mask, delta = self.update_block(net, inp, corr, coords1 - coords0,
                                                     corr_is_convc1=self.fuse_motion_corr)
             coords1 = coords1 + delta
-            predictions.append(self.image_padder.unpad(self.upsample_flow(coords1 - coords0, up_mask)))
+            up = (hip_upsample_flow if self.hip_upsample else self.upsample_flow)(coords1 - coords0, up_mask)
+            predictions.append(self.image_padder.unpad(up))
         return coords1 - coords0, predictions

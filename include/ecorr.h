@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 6
+#define ECORR_ABI_VERSION 7
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -111,6 +111,26 @@ int ecorr_forward_interpolate(const float* flow, int B, int h, int w, float* out
  * Replaces: utils/image_utils.py:10-47. */
 int ecorr_grid_sample_values(const float* pts, int64_t n, int h, int w, float* values, uint8_t* valid,
                              void* workspace, void* stream);
+
+/* ---- convex upsampling and the DSEC 16-bit PNG flow codec ---- */
+
+/* ERAFT.upsample_flow: flow float[N][2][H][W], mask float[N][576][H][W] (the update block's
+ * 0.25 * mask head) -> out float[N][2][8H][8W]; softmax over the 9 taps, convex combination of
+ * the zero-padded 3x3 window of 8 * flow.  Within a few ulp of the reference (device expf).
+ * Replaces: model/eraft.py:74-85. */
+int ecorr_upsample_flow(const float* flow, const float* mask, int N, int H, int W, float* out, void* stream);
+
+/* DSEC submission encoding: flow float[B][2][h][w] -> out uint16[B][h][w][3] =
+ * (u16)rint(flow * 128 + 2^15) with numpy's x86 float32 -> uint16 cast, channel 2 = 0.
+ * Bit-exact.  Replaces: utils/visualization.py:81-84 (before imageio.imwrite). */
+int ecorr_flow_to_png16(const float* flow, int B, int h, int w, uint16_t* out, void* stream);
+
+/* DSEC ground-truth decoding: in uint16[B][h][w][3] -> flow float[B][h][w][2] = (v - 2^15) / 128
+ * where channel 2 == 1 (else 0), valid uint8[B][h][w] = channel 2 == 1.  *bad (device int, zeroed
+ * by the caller) counts pixels whose channel 2 is neither 0 nor 1 (the reference asserts).
+ * Bit-exact.  Replaces: utils/dsec_utils.py:66-83 (after imageio.imread). */
+int ecorr_png16_to_flow(const uint16_t* in, int B, int h, int w, float* flow, uint8_t* valid, int* bad,
+                        void* stream);
 
 /* Tile shape of the pyramid storage (ECORR_TILE_H, ECORR_TILE_W). */
 int ecorr_pyramid_tile(int* tile_h, int* tile_w);

@@ -68,3 +68,71 @@ EXPORT void oracle_forward_interpolate(const float* flow, int B, int h, int w, f
     free(x);
     free(y);
 }
+
+/*
+ * Row 4 -- convex upsampling, /root/reference/model/eraft.py:74-85 (ERAFT.upsample_flow):
+ *   p_k = softmax_k(mask[n][64k + 8i + j][h][w]) as max, e_k = exp(x_k - max), s = sum_k e_k in
+ *   order, p_k = e_k / s (recip != 0: p_k = e_k * (1/s)); out = sum_k p_k * (8 flow)[window k] in
+ *   order from +0.  exp is libm expf, so agreement with ATen is within an ulp or two, not exact.
+ */
+EXPORT void oracle_upsample_flow(const float* flow, const float* mask, int N, int H, int W, int recip,
+                                 float* out) {
+    const long HW = (long)H * W;
+    for (int n = 0; n < N; ++n)
+        for (int h = 0; h < H; ++h)
+            for (int w = 0; w < W; ++w) {
+                float f8[2][9];
+                for (int c = 0; c < 2; ++c)
+                    for (int k = 0; k < 9; ++k) {
+                        const int y = h + k / 3 - 1, x = w + k % 3 - 1;
+                        f8[c][k] = (y >= 0 && y < H && x >= 0 && x < W)
+                                       ? 8.0f * flow[((long)n * 2 + c) * HW + (long)y * W + x] : 0.0f;
+                    }
+                for (int i = 0; i < 8; ++i)
+                    for (int j = 0; j < 8; ++j) {
+                        float m[9], mx, s = 0.0f;
+                        for (int k = 0; k < 9; ++k)
+                            m[k] = mask[((long)n * 576 + k * 64 + i * 8 + j) * HW + (long)h * W + w];
+                        mx = m[0];
+                        for (int k = 1; k < 9; ++k) mx = m[k] > mx ? m[k] : mx;
+                        for (int k = 0; k < 9; ++k) {
+                            m[k] = expf(m[k] - mx);
+                            s += m[k];
+                        }
+                        const float rs = 1.0f / s;
+                        for (int k = 0; k < 9; ++k) m[k] = recip ? m[k] * rs : m[k] / s;
+                        for (int c = 0; c < 2; ++c) {
+                            float acc = 0.0f;
+                            for (int k = 0; k < 9; ++k) acc += m[k] * f8[c][k];
+                            out[(((long)n * 2 + c) * 8 * H + 8 * h + i) * 8 * W + 8 * w + j] = acc;
+                        }
+                    }
+            }
+}
+
+/* DSEC PNG codec, utils/visualization.py:75-93 (encode) and utils/dsec_utils.py:66-83 (decode). */
+static uint16_t x86_f32_to_u16(float v) {
+    const int iv = (v >= -2147483648.0f && v < 2147483648.0f) ? (int)v : (int)0x80000000u;
+    return (uint16_t)(iv & 0xffff);
+}
+
+EXPORT void oracle_png16_encode(const float* flow, int B, int h, int w, uint16_t* out) {
+    const long HW = (long)h * w;
+    for (long q = 0; q < (long)B * HW; ++q) {
+        const long b = q / HW, p = q % HW;
+        for (int c = 0; c < 2; ++c)
+            out[3 * q + c] = x86_f32_to_u16(rintf(flow[(b * 2 + c) * HW + p] * 128.0f + 32768.0f));
+        out[3 * q + 2] = 0;
+    }
+}
+
+EXPORT int oracle_png16_decode(const uint16_t* in, long n, float* flow, uint8_t* valid) {
+    int bad = 0;
+    for (long q = 0; q < n; ++q) {
+        const int ok = in[3 * q + 2] == 1;
+        bad += in[3 * q + 2] > 1;
+        for (int c = 0; c < 2; ++c) flow[2 * q + c] = ok ? (float)((int)in[3 * q + c] - 32768) / 128.0f : 0.0f;
+        valid[q] = (uint8_t)ok;
+    }
+    return bad;
+}

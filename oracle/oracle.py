@@ -40,7 +40,14 @@ def lib():
         L.oracle_grid_sample_values.argtypes = [_f32p, _f32p, ctypes.c_void_p, ctypes.c_int, ctypes.c_long,
                                                  ctypes.c_int, ctypes.c_int, _f32p, ctypes.c_void_p]
         L.oracle_forward_interpolate.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p]
-        for fn in ("oracle_grid_sample_values", "oracle_forward_interpolate"):
+        L.oracle_upsample_flow.argtypes = [_f32p, _f32p] + [ctypes.c_int] * 4 + [_f32p]
+        _u16p = np.ctypeslib.ndpointer(dtype=np.uint16, flags="C_CONTIGUOUS")
+        _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+        L.oracle_png16_encode.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u16p]
+        L.oracle_png16_decode.argtypes = [_u16p, ctypes.c_long, _f32p, _u8p]
+        L.oracle_png16_decode.restype = ctypes.c_int
+        for fn in ("oracle_grid_sample_values", "oracle_forward_interpolate", "oracle_upsample_flow",
+                   "oracle_png16_encode"):
             getattr(L, fn).restype = None
         for fn in ("oracle_corr_level0", "oracle_avg_pool2", "oracle_lookup",
                    "oracle_bilinear_sampler", "oracle_coords_grid"):
@@ -162,3 +169,34 @@ def grid_sample_values(inp, h, w):
     lib().oracle_grid_sample_values(inp[0].copy(), inp[1].copy(), z.ctypes.data, 1, n, h, w, values,
                                     valid.ctypes.data)
     return values, valid.astype(bool)
+
+
+def upsample_flow(flow, mask):
+    """eraft.py:74-85: flow [N,2,H,W], mask [N,576,H,W] -> [N,2,8H,8W] (libm expf)."""
+    flow, mask = _c(flow), _c(mask)
+    N, _, H, W = flow.shape
+    out = np.empty((N, 2, 8 * H, 8 * W), dtype=np.float32)
+    lib().oracle_upsample_flow(flow, mask, N, H, W, 0, out)
+    return out
+
+
+def flow_to_png16(flow):
+    """visualization.py:81-84: flow [2,h,w] or [B,2,h,w] -> uint16 [(B,) h, w, 3]."""
+    f = _c(flow)
+    single = f.ndim == 3
+    if single:
+        f = f[None]
+    B, _, h, w = f.shape
+    out = np.empty((B, h, w, 3), dtype=np.uint16)
+    lib().oracle_png16_encode(f, B, h, w, out)
+    return out[0] if single else out
+
+
+def flow_16bit_to_float(png):
+    """dsec_utils.py:66-83: uint16 [h,w,3] -> (flow [h,w,2] float32, valid [h,w] bool, n_bad)."""
+    png = np.ascontiguousarray(png, dtype=np.uint16)
+    h, w, _ = png.shape
+    flow = np.empty((h, w, 2), dtype=np.float32)
+    valid = np.empty((h, w), dtype=np.uint8)
+    bad = lib().oracle_png16_decode(png, h * w, flow, valid)
+    return flow, valid.astype(bool), bad

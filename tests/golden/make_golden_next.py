@@ -11,6 +11,12 @@ on torch-CPU; inputs are drawn from tests/prng.py and stored alongside the refer
                     fields (sub-pixel, large/out-of-image, converging = many collisions, integer =
                     floor == ceil, NaN/inf, 3-D input) and grid_sample_values (:10-47) on scattered
                     points incl. the empty set.
+  next_flow.npz     model/eraft.py ERAFT.upsample_flow (:74-85) on PRNG flows/masks (mask scales
+                    0.25 .. 30: flat to one-hot softmax); the DSEC PNG codec: the submission
+                    array of utils/visualization.py:81-84 (that module is not importable here --
+                    its loader import needs h5py -- so its three numpy lines are evaluated as
+                    written) and utils/dsec_utils.py flow_16bit_to_float (:66-83, imported),
+                    incl. out-of-range / NaN / tie values and the assertion case.
 """
 import os
 import sys
@@ -24,6 +30,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import prng  # noqa: E402
+from model.eraft import ERAFT  # noqa: E402  (reference)
+from utils.dsec_utils import flow_16bit_to_float  # noqa: E402  (reference)
 from utils.image_utils import forward_interpolate_pytorch, grid_sample_values  # noqa: E402  (reference)
 
 torch.set_num_threads(8)
@@ -66,9 +74,56 @@ def splat_cases():
     return out
 
 
+UPSAMPLE_CASES = {"up_small": (2, 6, 8, 1.0, 300), "up_dsec_crop": (1, 15, 20, 0.75, 310),
+                  "up_onehot": (1, 4, 5, 30.0, 320), "up_flat": (1, 3, 7, 0.01, 330)}
+
+
+def flow_cases():
+    out = {}
+    for k, (N, H, W, mscale, seed) in UPSAMPLE_CASES.items():
+        flow = prng.normal(seed, (N, 2, H, W), 4.0)
+        mask = prng.normal(seed + 1, (N, 576, H, W), mscale)
+        ref = ERAFT.upsample_flow(None, torch.from_numpy(flow), torch.from_numpy(mask)).numpy()
+        out[f"{k}/shape"] = np.array([N, H, W, seed], dtype=np.int64)
+        out[f"{k}/mscale"] = np.array(mscale, dtype=np.float64)
+        out[f"{k}/out"] = ref
+    # encoder: flow [2, h, w] -> the uint16 [h, w, 3] array written to the submission PNG
+    f = prng.normal(340, (2, 24, 32), 40.0)
+    special = np.array([0.5 / 128, 1.5 / 128, -0.5 / 128, 2.5 / 128, 255.99, 256.0, -256.0, -300.0,
+                        600.0, 1e9, -1e9, np.nan, np.inf, -np.inf, 1e-30, -0.0], dtype=np.float32)
+    f.reshape(-1)[:special.size] = special
+    for name, flow in {"enc_rand": f, "enc_small": prng.normal(341, (2, 5, 7), 3.0)}.items():
+        _, h, w = flow.shape
+        with np.errstate(invalid="ignore"):
+            flow_map = np.rint(flow * 128 + 2 ** 15)                       # visualization.py:82
+            flow_map = flow_map.astype(np.uint16).transpose(1, 2, 0)        # :83
+        flow_map = np.concatenate((flow_map, np.zeros((h, w, 1), dtype=np.uint16)), axis=-1)   # :84
+        out[f"{name}/flow"] = flow
+        out[f"{name}/png"] = flow_map
+    # decoder
+    u = (prng.uniform(350, (40, 48, 3)) * 65536).astype(np.int64).clip(0, 65535).astype(np.uint16)
+    u[..., 2] = (prng.uniform(351, (40, 48)) < 0.7).astype(np.uint16)
+    fm, valid = flow_16bit_to_float(u.copy())
+    out["dec/png"] = u
+    out["dec/flow"] = fm
+    out["dec/valid"] = valid
+    bad = u.copy()
+    bad[3, 4, 2] = 2
+    try:
+        flow_16bit_to_float(bad)
+        raised = False
+    except AssertionError:
+        raised = True
+    out["dec_bad/png"] = bad
+    out["dec_bad/raises"] = np.array(raised)
+    return out
+
+
 def main():
     np.savez_compressed(os.path.join(HERE, "next_splat.npz"), **splat_cases())
     print("wrote next_splat.npz")
+    np.savez_compressed(os.path.join(HERE, "next_flow.npz"), **flow_cases())
+    print("wrote next_flow.npz")
 
 
 if __name__ == "__main__":

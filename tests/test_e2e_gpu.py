@@ -34,14 +34,15 @@ def epe(a, b):
     return float(np.mean(np.sqrt(np.sum(d * d, axis=1))))
 
 
-def _run(z, corr_cls=None, fuse=False):
+def _run(z, corr_cls=None, fuse=False, hip_up=False):
     import eraft_amd.network as nw
     H, W, bins, seed = int(z["H"]), int(z["W"]), int(z["bins"]), int(z["seed"])
     saved = nw.CorrBlock
     if corr_cls is not None:
         nw.CorrBlock = corr_cls
     try:
-        net = nw.ERAFT({"subtype": str(z["subtype"])}, n_first_channels=bins, fuse_motion_corr=fuse)
+        net = nw.ERAFT({"subtype": str(z["subtype"])}, n_first_channels=bins, fuse_motion_corr=fuse,
+                       hip_upsample=hip_up)
         net.load_state_dict(make_state_dict(net.state_dict()))
         net = net.eval().cuda()
         im1 = torch.from_numpy(prng.normal(seed, (1, bins, H, W))).cuda()
@@ -94,3 +95,22 @@ def test_e2e_fused_motion_corr(path):
           f"vs unfused (same GPU) low {epe(low, base_low):.3g} up {epe(up, base_up):.3g}")
     assert e_low <= EPE_TOL
     assert e_up <= EPE_TOL
+
+
+@pytest.mark.parametrize("path", CASES, ids=lambda p: os.path.basename(p)[:-4])
+def test_e2e_all_native(path):
+    """Every §8 kernel on the path: HIP CorrBlock build, fused lookup + convc1 (row 1) and the HIP
+    convex upsampling (row 4) -- same EPE bar against the reference."""
+    if not torch.cuda.is_available():
+        pytest.fail("no HIP device visible")
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    z = np.load(path)
+    low, (_, up) = _run(z, fuse=True, hip_up=True)
+    base_low, (_, base_up) = _run(z, fuse=True)
+    e_low, e_up = epe(low, z["flow_low"]), epe(up, z["flow_up"])
+    print(f"{os.path.basename(path)} all-native: EPE vs reference low {e_low:.3g} px, up {e_up:.3g} px | "
+          f"HIP vs ATen upsampling (same GPU) up {epe(up, base_up):.3g}")
+    assert e_low <= EPE_TOL
+    assert e_up <= EPE_TOL
+    assert epe(low, base_low) <= 1e-6   # upsampling does not feed back into the iteration

@@ -1,0 +1,92 @@
+"""GPU parity of SURVEY §8f row 4 (upsample.hip) through the C ABI: convex upsampling within a few
+ulp of the reference (device expf; tolerance in the test) and the DSEC PNG codec bit-exact."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import prng
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+UPSAMPLE_TOL = 2e-6   # max|got - ref| / rms(ref)
+
+
+@pytest.fixture(scope="module")
+def ea():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    import eraft_amd
+    eraft_amd.lib()
+    return eraft_amd
+
+
+@pytest.fixture(scope="module")
+def flowz():
+    return np.load(os.path.join(GOLD, "next_flow.npz"))
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def test_upsample_goldens(ea, flowz):
+    from test_oracle_next import upsample_inputs
+    names = sorted(k.split("/")[0] for k in flowz.files if k.startswith("up_") and k.endswith("/out"))
+    for k in names:
+        flow, mask = upsample_inputs(flowz, k)
+        got = ea.upsample_flow(_dev(flow), _dev(mask)).cpu().numpy()
+        assert oracle.normwise_err(got, flowz[f"{k}/out"]) <= UPSAMPLE_TOL, k
+
+
+@pytest.mark.parametrize("N,H,W,ms", [(16, 60, 80, 0.5), (4, 92, 160, 1.0), (3, 7, 9, 20.0)])
+def test_upsample_vs_oracle(ea, N, H, W, ms):
+    flow = prng.normal(400 + H, (N, 2, H, W), 3.0)
+    mask = prng.normal(401 + H, (N, 576, H, W), ms)
+    got = ea.upsample_flow(_dev(flow), _dev(mask)).cpu().numpy()
+    ref = oracle.upsample_flow(flow, mask)
+    assert oracle.normwise_err(got, ref) <= UPSAMPLE_TOL
+    # with exp out of the picture (a one-hot mask) the convex combination is exact: the output is
+    # 8 x the flow of the selected tap
+    if ms >= 20.0:
+        assert np.isfinite(got).all()
+
+
+def test_upsample_matches_torch_expression(ea):
+    # the reference's own expression on this GPU (ATen ops), same inputs
+    import torch.nn.functional as F
+    N, H, W = 2, 20, 28
+    flow = _dev(prng.normal(410, (N, 2, H, W), 3.0))
+    mask = _dev(prng.normal(411, (N, 576, H, W), 1.0))
+    m = torch.softmax(mask.view(N, 1, 9, 8, 8, H, W), dim=2)
+    up = F.unfold(8 * flow, [3, 3], padding=1).view(N, 2, 9, 1, 1, H, W)
+    ref = torch.sum(m * up, dim=2).permute(0, 1, 4, 2, 5, 3).reshape(N, 2, 8 * H, 8 * W)
+    got = ea.upsample_flow(flow, mask)
+    assert oracle.normwise_err(got.cpu().numpy(), ref.cpu().numpy()) <= UPSAMPLE_TOL
+
+
+def test_png16_goldens(ea, flowz):
+    for k in ("enc_rand", "enc_small"):
+        got = ea.flow_to_png16(_dev(flowz[f"{k}/flow"]))
+        assert got.dtype == torch.uint16
+        assert np.array_equal(got.cpu().numpy(), flowz[f"{k}/png"]), k
+    flow, valid = ea.flow_16bit_to_float(_dev(flowz["dec/png"]))
+    assert np.array_equal(valid.cpu().numpy(), flowz["dec/valid"])
+    assert np.array_equal(flow.cpu().numpy().astype(np.float64), flowz["dec/flow"])
+    with pytest.raises(AssertionError):
+        ea.flow_16bit_to_float(_dev(flowz["dec_bad/png"]))
+
+
+def test_png16_roundtrip_full_res(ea):
+    # DSEC full resolution, batched: decode(encode(f)) = rint(128 f) / 128 on the valid pixels
+    f = prng.normal(420, (4, 2, 480, 640), 30.0)
+    png = ea.flow_to_png16(_dev(f))
+    assert np.array_equal(png.cpu().numpy(), oracle.flow_to_png16(f))
+    png[..., 2] = 1
+    back, valid = ea.flow_16bit_to_float(png[1])
+    assert bool(valid.all())
+    want = (np.rint(f[1] * 128 + 32768) - 32768) / 128
+    assert np.array_equal(back.cpu().numpy(), want.transpose(1, 2, 0).astype(np.float32))

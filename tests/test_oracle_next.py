@@ -33,3 +33,34 @@ def test_grid_sample_values_oracle_bit_exact(splat):
         values, valid = oracle.grid_sample_values(splat[f"{k}/input"], h, w)
         assert oracle.same_bits(values, splat[f"{k}/values"]), k
         assert np.array_equal(valid, splat[f"{k}/valid"]), k
+
+
+@pytest.fixture(scope="module")
+def flowz():
+    return np.load(os.path.join(GOLD, "next_flow.npz"))
+
+
+def upsample_inputs(z, k):
+    import prng
+    N, H, W, seed = (int(v) for v in z[f"{k}/shape"])
+    return (prng.normal(seed, (N, 2, H, W), 4.0),
+            prng.normal(seed + 1, (N, 576, H, W), float(z[f"{k}/mscale"])))
+
+
+def test_upsample_oracle_vs_reference(flowz):
+    # libm expf vs ATen's vectorized exp: a few ulp, never more (tolerance in units of the output rms)
+    for k in _cases(flowz, "up_", "out"):
+        flow, mask = upsample_inputs(flowz, k)
+        ref = flowz[f"{k}/out"]
+        got = oracle.upsample_flow(flow, mask)
+        assert oracle.normwise_err(got, ref) <= 2e-6, k
+
+
+def test_png16_codec_oracle_bit_exact(flowz):
+    for k in ("enc_rand", "enc_small"):
+        assert np.array_equal(oracle.flow_to_png16(flowz[f"{k}/flow"]), flowz[f"{k}/png"]), k
+    flow, valid, bad = oracle.flow_16bit_to_float(flowz["dec/png"])
+    assert bad == 0
+    assert np.array_equal(valid, flowz["dec/valid"])
+    assert np.array_equal(flow.astype(np.float64), flowz["dec/flow"])   # exact in float32
+    assert bool(flowz["dec_bad/raises"]) and oracle.flow_16bit_to_float(flowz["dec_bad/png"])[2] == 1
