@@ -226,6 +226,50 @@ def measure_upsample(B, H, W, device, reps=5):
             "work_per_launch": f"{nbytes:.4g} B (mask + flow in, 8x flow out)"}
 
 
+def measure_voxel(device, n=1_000_000, C=15, H=480, W=640, reps=5):
+    """DSEC event -> voxel grid (dsec_utils.py:26-64) for one 100 ms window of
+    n synthetic events at full resolution, normalized -- ours (voxel.hip: prep, stable radix sort,
+    ordered gather, normalization) vs the reference's ATen op sequence (oracle/torch_ref.py) on this
+    GPU and on one host core (main.py pins torch to one thread)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch_ref
+    import eraft_amd
+    g = torch.Generator(device=device).manual_seed(8)
+    t = torch.sort(torch.rand((n,), generator=g, device=device) * 1e5).values
+    ev = {"p": (torch.rand((n,), generator=g, device=device) < 0.5).float(), "t": t - t[0],
+          "x": torch.rand((n,), generator=g, device=device) * (W + 2) - 1.5,
+          "y": torch.rand((n,), generator=g, device=device) * (H + 2) - 1.5}
+    vg = eraft_amd.VoxelGrid((C, H, W), normalize=True)
+    stream = torch.cuda.current_stream(device)
+
+    def gpu_ms(fn):
+        ts = []
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return sorted(ts[1:])[len(ts[1:]) // 2]
+
+    ours = gpu_ms(lambda: vg.convert(ev))
+    ref_gpu = gpu_ms(lambda: torch_ref.voxel_grid_dsec(ev, C, H, W))
+    evc = {k: v.cpu() for k, v in ev.items()}
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    t0 = time.perf_counter()
+    torch_ref.voxel_grid_dsec(evc, C, H, W)
+    ref_cpu = (time.perf_counter() - t0) * 1e3
+    torch.set_num_threads(nt)
+    return {"ms_per_call": round(ours, 4), "events": n, "grid": [C, H, W],
+            "events_per_s": round(n / (ours * 1e-3), 1),
+            "reference_ops_on_gpu_ms": round(ref_gpu, 3), "reference_ops_on_1_cpu_core_ms": round(ref_cpu, 1),
+            "speedup_vs_reference_gpu": round(ref_gpu / ours, 2),
+            "note": "accumulated grid bit-exact with the reference's serial fold (the reference on a "
+                    "GPU uses float atomics: not reproducible); normalization within 1e-6"}
+
+
 def pmc_traffic(kernel_prefix):
     """HBM bytes per dispatch of the dominant kernel from the committed PMC summary of this same
     bench command (profiles/latest_pmc.json, written by tools/pmc_summary.py), else None."""
@@ -361,7 +405,8 @@ def main():
         with torch.no_grad():
             res["next_rows"] = {"lookup_conv1x1_relu": measure_fused_convc1(make_block(), coords, B, H, W, device),
                                 "forward_interpolate": measure_forward_interpolate(B, H, W, device),
-                                "upsample_flow": measure_upsample(B, H, W, device)}
+                                "upsample_flow": measure_upsample(B, H, W, device),
+                                "voxel_grid_dsec": measure_voxel(device)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(B, D, H, W, iters, a.cpu_seconds)
     if rank == 0:

@@ -11,7 +11,9 @@ from .corr import CorrBlock
 from .utils import bilinear_sampler, coords_grid
 from .image_utils import forward_interpolate_pytorch, grid_sample_values
 from .flow import flow_16bit_to_float, flow_to_png16, upsample_flow
+from .voxel import EventSequenceToVoxelGrid_Pytorch, VoxelGrid
 from ._lib import LIB_PATH, lib
 
 __all__ = ["CorrBlock", "bilinear_sampler", "coords_grid", "forward_interpolate_pytorch", "grid_sample_values",
-           "upsample_flow", "flow_to_png16", "flow_16bit_to_float", "LIB_PATH", "lib"]
+           "upsample_flow", "flow_to_png16", "flow_16bit_to_float",
+           "VoxelGrid", "EventSequenceToVoxelGrid_Pytorch", "LIB_PATH", "lib"]

@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -57,6 +57,12 @@ SYMBOLS = {
     "ecorr_flow_to_png16": (_i, [_p, _i, _i, _i, _p, _p]),
     # (in_u16, B, h, w, flow, valid, bad, stream)
     "ecorr_png16_to_flow": (_i, [_p, _i, _i, _i, _p, _p, _p, _p]),
+    # (dsec, n, C, H, W, bytes*)
+    "ecorr_voxel_workspace_size": (_i, [_i, _i64, _i, _i, _i, ctypes.POINTER(_i64)]),
+    # (p, t, x, y, n, C, H, W, normalize, voxel, workspace, stream)
+    "ecorr_voxel_grid_dsec": (_i, [_p, _p, _p, _p, _i64, _i, _i, _i, _i, _p, _p, _p]),
+    # (events, n, C, H, W, normalize, voxel, bad_index, workspace, stream)
+    "ecorr_voxel_grid_mvsec": (_i, [_p, _i64, _i, _i, _i, _i, _p, _p, _p, _p]),
 }
 
 

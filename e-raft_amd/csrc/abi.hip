@@ -229,3 +229,33 @@ ECORR_EXPORT int ecorr_png16_to_flow(const uint16_t* in, int B, int h, int w, fl
     if (!in || !flow || !valid || !bad || B <= 0 || h <= 0 || w <= 0) return ECORR_EINVAL;
     return launch_png16_decode(in, B, h, w, flow, valid, bad, (hipStream_t)stream);
 }
+
+namespace {
+
+bool voxel_dims_ok(int64_t n, int C, int H, int W) {
+    // keys (extended grid for DSEC) must stay below 2^32 - 1; event indices are int32
+    return n >= 1 && n <= 0x7fffffff && C > 0 && H > 0 && W > 0 &&
+           (int64_t)(C + 1) * (H + 1) * (W + 1) < 0xffffffffLL;
+}
+
+}  // namespace
+
+ECORR_EXPORT int ecorr_voxel_workspace_size(int dsec, int64_t n, int C, int H, int W, int64_t* bytes) {
+    if (!bytes || !voxel_dims_ok(n, C, H, W)) return ECORR_EINVAL;
+    return voxel_workspace_bytes(dsec != 0, n, C, H, W, bytes);
+}
+
+ECORR_EXPORT int ecorr_voxel_grid_dsec(const float* p, const float* t, const float* x, const float* y, int64_t n,
+                                       int C, int H, int W, int normalize, float* voxel, void* workspace,
+                                       void* stream) {
+    if (!p || !t || !x || !y || !voxel || !workspace || !voxel_dims_ok(n, C, H, W)) return ECORR_EINVAL;
+    return launch_voxel(true, p, t, x, y, nullptr, n, C, H, W, normalize, voxel, nullptr, workspace,
+                        (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_voxel_grid_mvsec(const double* events, int64_t n, int C, int H, int W, int normalize,
+                                        float* voxel, int* bad_index, void* workspace, void* stream) {
+    if (!events || !voxel || !bad_index || !workspace || !voxel_dims_ok(n, C, H, W)) return ECORR_EINVAL;
+    return launch_voxel(false, nullptr, nullptr, nullptr, nullptr, events, n, C, H, W, normalize, voxel, bad_index,
+                        workspace, (hipStream_t)stream);
+}

@@ -68,6 +68,12 @@ int launch_png16_encode(const float* flow, int B, int h, int w, uint16_t* out, h
 int launch_png16_decode(const uint16_t* in, int B, int h, int w, float* flow, uint8_t* valid, int* bad,
                         hipStream_t stream);
 
+uint32_t voxel_key_range(bool dsec, int C, int H, int W);
+int voxel_workspace_bytes(bool dsec, int64_t n, int C, int H, int W, int64_t* bytes);
+int launch_voxel(bool dsec, const float* p, const float* t, const float* x, const float* y, const double* ev,
+                 int64_t n, int C, int H, int W, int normalize, float* voxel, int* bad, void* workspace,
+                 hipStream_t stream);
+
 int64_t splat_workspace_bytes(bool flow_mode, int B, int64_t n, int h, int w);
 int launch_splat(bool flow_mode, const float* pts, int B, int64_t n, int h, int w, float* values, uint8_t* valid,
                  void* workspace, hipStream_t stream);

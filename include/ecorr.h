@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 7
+#define ECORR_ABI_VERSION 8
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -131,6 +131,27 @@ int ecorr_flow_to_png16(const float* flow, int B, int h, int w, uint16_t* out, v
  * Bit-exact.  Replaces: utils/dsec_utils.py:66-83 (after imageio.imread). */
 int ecorr_png16_to_flow(const uint16_t* in, int B, int h, int w, float* flow, uint8_t* valid, int* bad,
                         void* stream);
+
+/* ---- event stream -> voxel grid ----
+ * The accumulated grid is bit-exact with the reference's single-threaded serial fold (stable sort
+ * of the events by base cell + ordered per-cell gather); normalization (nonzero mean / unbiased
+ * std) agrees within an ulp or two.  n >= 1 events; voxel float[C][H][W]. */
+
+/* Workspace bytes for n events on a C x H x W grid (dsec != 0: ecorr_voxel_grid_dsec, else
+ * ecorr_voxel_grid_mvsec). */
+int ecorr_voxel_workspace_size(int dsec, int64_t n, int C, int H, int W, int64_t* bytes);
+
+/* VoxelGrid.convert: p, t, x, y float[n] (t ascending), trilinear in (x, y, t).
+ * Replaces: utils/dsec_utils.py:26-64 (as called by loader/loader_dsec.py:245-257). */
+int ecorr_voxel_grid_dsec(const float* p, const float* t, const float* x, const float* y, int64_t n, int C,
+                          int H, int W, int normalize, float* voxel, void* workspace, void* stream);
+
+/* EventSequenceToVoxelGrid_Pytorch: events double[n][4] = (t, x, y, p), bilinear in t.
+ * *bad_index (device int, zeroed by the caller) becomes nonzero where the reference's index_add_
+ * would raise (an index outside the grid); the grid is then undefined.
+ * Replaces: utils/transformers.py:36-126. */
+int ecorr_voxel_grid_mvsec(const double* events, int64_t n, int C, int H, int W, int normalize, float* voxel,
+                           int* bad_index, void* workspace, void* stream);
 
 /* Tile shape of the pyramid storage (ECORR_TILE_H, ECORR_TILE_W). */
 int ecorr_pyramid_tile(int* tile_h, int* tile_w);

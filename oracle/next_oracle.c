@@ -136,3 +136,97 @@ EXPORT int oracle_png16_decode(const uint16_t* in, long n, float* flow, uint8_t*
     }
     return bad;
 }
+
+/*
+ * Row 3 -- event -> voxel grid.
+ *
+ * DSEC, utils/dsec_utils.py:26-64 (VoxelGrid.convert; the loader passes fp32 p, t, x, y,
+ * loader/loader_dsec.py:245-257): t_norm = ((C-1) * (t - t[0])) / (t[-1] - t[0]); x0 = x.int()
+ * (truncation, x86 cvttss2si: NaN / out of int32 -> INT_MIN); value = 2p - 1; for xlim in {x0,
+ * x0+1} / ylim in {y0, y0+1} / tlim in {t0, t0+1} (that nesting = the pass order): in-bounds
+ * entries add value * (1-|xlim-x|) * (1-|ylim-y|) * (1-|tlim-t_norm|) (left to right, fp32) with
+ * put_(accumulate=True) -- serial in event order, since main.py:2-5 pins torch to one thread.
+ *
+ * MVSEC, utils/transformers.py:36-126 (EventSequenceToVoxelGrid_Pytorch, float64 events
+ * [n][4] = t, x, y, p): ts = (bins-1) * (t - t0) / dT (f64, dT = 1 if 0); xs, ys = .long();
+ * pol = float(p), 0 -> -1; tis = floor(ts); dts = ts - tis; left = pol * (1 - float(dts)),
+ * right = pol * float(dts); index_add_ (serial) of all left values at xs + ys W + tis W H where
+ * 0 <= tis < bins, then all right values at +W H where 0 <= tis and tis + 1 < bins.  An index
+ * outside the grid raises in the reference (returned here as nonzero).
+ *
+ * normalize (both, dsec_utils.py:55-62 / transformers.py:117-124): over the nonzero cells,
+ * mean (sum in double, rounded), std (unbiased, double two-pass, rounded); v = (v - mean) / std,
+ * or v - mean when std == 0.  ATen reduces in its own order, so normalized values agree within a
+ * few ulp; the accumulated grid itself is bit-exact.
+ */
+static int x86_f32_to_i32(float v) {
+    return (v >= -2147483648.0f && v < 2147483648.0f) ? (int)v : (int)0x80000000u;
+}
+
+static long long x86_f64_to_i64(double v) {
+    return (v >= -9223372036854775808.0 && v < 9223372036854775808.0) ? (long long)v : (long long)(1ULL << 63);
+}
+
+static void voxel_normalize(float* g, long n) {
+    long cnt = 0;
+    double sum = 0.0;
+    for (long i = 0; i < n; ++i)
+        if (g[i] != 0.0f) { ++cnt; sum += g[i]; }
+    if (cnt == 0) return;
+    const double m64 = sum / (double)cnt;
+    double m2 = 0.0;
+    for (long i = 0; i < n; ++i)
+        if (g[i] != 0.0f) { const double d = g[i] - m64; m2 += d * d; }
+    const float mean = (float)m64;
+    const float std = cnt > 1 ? (float)sqrt(m2 / (double)(cnt - 1)) : NAN;
+    for (long i = 0; i < n; ++i)
+        if (g[i] != 0.0f) g[i] = std > 0.0f ? (g[i] - mean) / std : g[i] - mean;
+}
+
+EXPORT void oracle_voxel_dsec(const float* p, const float* t, const float* x, const float* y, long n, int C,
+                              int H, int W, int normalize, float* out) {
+    const long HW = (long)H * W;
+    memset(out, 0, sizeof(float) * (size_t)(C * HW));
+    const float dt = t[n - 1] - t[0];
+    float* tn = (float*)malloc(sizeof(float) * (size_t)n);
+    for (long e = 0; e < n; ++e) tn[e] = ((float)(C - 1) * (t[e] - t[0])) / dt;
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b)
+            for (int c = 0; c < 2; ++c)
+                for (long e = 0; e < n; ++e) {
+                    const int xl = x86_f32_to_i32(x[e]) + a, yl = x86_f32_to_i32(y[e]) + b,
+                              tl = x86_f32_to_i32(tn[e]) + c;
+                    if (!(xl < W && xl >= 0 && yl < H && yl >= 0 && tl >= 0 && tl < C)) continue;
+                    const float v = 2.0f * p[e] - 1.0f;
+                    const float wgt = ((v * (1.0f - fabsf((float)xl - x[e]))) * (1.0f - fabsf((float)yl - y[e]))) *
+                                      (1.0f - fabsf((float)tl - tn[e]));
+                    out[(long)tl * HW + (long)yl * W + xl] += wgt;
+                }
+    free(tn);
+    if (normalize) voxel_normalize(out, C * HW);
+}
+
+EXPORT int oracle_voxel_mvsec(const double* ev, long n, int C, int H, int W, int normalize, float* out) {
+    const long HW = (long)H * W, CHW = C * HW;
+    memset(out, 0, sizeof(float) * (size_t)CHW);
+    const double first = ev[0], last = ev[4 * (n - 1)];
+    double dT = last - first;
+    if (dT == 0.0) dT = 1.0;
+    int bad = 0;
+    for (int pass = 0; pass < 2; ++pass)
+        for (long e = 0; e < n; ++e) {
+            const double ts = (double)(C - 1) * (ev[4 * e] - first) / dT;
+            const long long xs = x86_f64_to_i64(ev[4 * e + 1]), ys = x86_f64_to_i64(ev[4 * e + 2]);
+            float pol = (float)ev[4 * e + 3];
+            if (pol == 0.0f) pol = -1.0f;
+            const double tis = floor(ts);
+            const float dts = (float)(ts - tis);
+            const int ok = pass == 0 ? (tis < C && tis >= 0) : (tis + 1 < C && tis >= 0);
+            if (!ok) continue;
+            const long long idx = xs + ys * W + (x86_f64_to_i64(tis) + pass) * HW;
+            if (idx < 0 || idx >= CHW) { bad = 1; continue; }
+            out[idx] += pass == 0 ? pol * (1.0f - dts) : pol * dts;
+        }
+    if (normalize && !bad) voxel_normalize(out, CHW);
+    return bad;
+}

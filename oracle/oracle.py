@@ -46,6 +46,11 @@ def lib():
         L.oracle_png16_encode.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u16p]
         L.oracle_png16_decode.argtypes = [_u16p, ctypes.c_long, _f32p, _u8p]
         L.oracle_png16_decode.restype = ctypes.c_int
+        _f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+        L.oracle_voxel_dsec.argtypes = [_f32p] * 4 + [ctypes.c_long] + [ctypes.c_int] * 4 + [_f32p]
+        L.oracle_voxel_dsec.restype = None
+        L.oracle_voxel_mvsec.argtypes = [_f64p, ctypes.c_long] + [ctypes.c_int] * 4 + [_f32p]
+        L.oracle_voxel_mvsec.restype = ctypes.c_int
         for fn in ("oracle_grid_sample_values", "oracle_forward_interpolate", "oracle_upsample_flow",
                    "oracle_png16_encode"):
             getattr(L, fn).restype = None
@@ -200,3 +205,19 @@ def flow_16bit_to_float(png):
     valid = np.empty((h, w), dtype=np.uint8)
     bad = lib().oracle_png16_decode(png, h * w, flow, valid)
     return flow, valid.astype(bool), bad
+
+
+def voxel_dsec(p, t, x, y, C, H, W, normalize):
+    """dsec_utils.py:26-64 -> [C, H, W] float32 (serial fold; normalization in double)."""
+    p, t, x, y = (_c(v).reshape(-1) for v in (p, t, x, y))
+    out = np.empty((C, H, W), dtype=np.float32)
+    lib().oracle_voxel_dsec(p, t, x, y, p.size, C, H, W, int(bool(normalize)), out)
+    return out
+
+
+def voxel_mvsec(events, C, H, W, normalize):
+    """transformers.py:36-126: events [n, 4] float64 -> ([C, H, W] float32, bad_index)."""
+    ev = np.ascontiguousarray(events, dtype=np.float64)
+    out = np.empty((C, H, W), dtype=np.float32)
+    bad = lib().oracle_voxel_mvsec(ev, ev.shape[0], C, H, W, int(bool(normalize)), out)
+    return out, bad

@@ -88,3 +88,25 @@ def forward_interpolate_pytorch(flow_in):
         flow_new[i, 0] = grid_sample_values(torch.stack([x1[i], y1[i], dx[i]]), h, w)[0]
         flow_new[i, 1] = grid_sample_values(torch.stack([x1[i], y1[i], dy[i]]), h, w)[0]
     return flow_new
+
+
+def voxel_grid_dsec(events, C, H, W, normalize=True):
+    """utils/dsec_utils.py:26-64 (VoxelGrid.convert), same ATen ops in the same order."""
+    grid = torch.zeros((C, H, W), dtype=torch.float, device=events["p"].device)
+    t = events["t"]
+    t = (C - 1) * (t - t[0]) / (t[-1] - t[0])
+    x0, y0, t0 = events["x"].int(), events["y"].int(), t.int()
+    value = 2 * events["p"] - 1
+    for xl in (x0, x0 + 1):
+        for yl in (y0, y0 + 1):
+            for tl in (t0, t0 + 1):
+                m = (xl < W) & (xl >= 0) & (yl < H) & (yl >= 0) & (tl >= 0) & (tl < C)
+                w = value * (1 - (xl - events["x"]).abs()) * (1 - (yl - events["y"]).abs()) * (1 - (tl - t).abs())
+                idx = H * W * tl.long() + W * yl.long() + xl.long()
+                grid.put_(idx[m], w[m], accumulate=True)
+    if normalize:
+        nz = torch.nonzero(grid, as_tuple=True)
+        if nz[0].size()[0] > 0:
+            mean, std = grid[nz].mean(), grid[nz].std()
+            grid[nz] = (grid[nz] - mean) / std if std > 0 else grid[nz] - mean
+    return grid

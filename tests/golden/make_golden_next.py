@@ -17,6 +17,11 @@ on torch-CPU; inputs are drawn from tests/prng.py and stored alongside the refer
                     its loader import needs h5py -- so its three numpy lines are evaluated as
                     written) and utils/dsec_utils.py flow_16bit_to_float (:66-83, imported),
                     incl. out-of-range / NaN / tie values and the assertion case.
+  next_voxel.npz    utils/dsec_utils.py VoxelGrid.convert (:26-64) and utils/transformers.py
+                    EventSequenceToVoxelGrid_Pytorch (:36-126) on prng.dsec_events /
+                    prng.mvsec_events (seeds stored), normalize off and on, with torch pinned to
+                    one thread as main.py:2-5 does; edge cases: constant timestamps, NaN
+                    coordinates, one hot pixel, an out-of-grid MVSEC index (raises).
 """
 import os
 import sys
@@ -30,8 +35,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import prng  # noqa: E402
+from voxel_cases import DSEC_VOXEL, MVSEC_VOXEL, dsec_case, mvsec_case  # noqa: E402
 from model.eraft import ERAFT  # noqa: E402  (reference)
-from utils.dsec_utils import flow_16bit_to_float  # noqa: E402  (reference)
+from utils.dsec_utils import VoxelGrid, flow_16bit_to_float  # noqa: E402  (reference)
+from utils.transformers import EventSequenceToVoxelGrid_Pytorch  # noqa: E402  (reference)
 from utils.image_utils import forward_interpolate_pytorch, grid_sample_values  # noqa: E402  (reference)
 
 torch.set_num_threads(8)
@@ -119,11 +126,42 @@ def flow_cases():
     return out
 
 
+class _Seq:
+    pass
+
+
+def voxel_cases():
+    torch.set_num_threads(1)   # main.py:2-5
+    out = {}
+    for k, (n, C, H, W, seed) in DSEC_VOXEL.items():
+        p, t, x, y = dsec_case(k, n, H, W, seed)
+        out[f"{k}/shape"] = np.array([n, C, H, W, seed], dtype=np.int64)
+        for norm in (0, 1):
+            ev = {"p": torch.from_numpy(p.copy()), "t": torch.from_numpy(t.copy()),
+                  "x": torch.from_numpy(x.copy()), "y": torch.from_numpy(y.copy())}
+            out[f"{k}/norm{norm}"] = VoxelGrid((C, H, W), normalize=bool(norm)).convert(ev).numpy()
+    for k, (n, C, H, W, seed) in MVSEC_VOXEL.items():
+        ev = mvsec_case(k, n, H, W, seed)
+        out[f"{k}/shape"] = np.array([n, C, H, W, seed], dtype=np.int64)
+        for norm in (0, 1):
+            s = _Seq()
+            s.features, s.image_width, s.image_height = ev.copy(), W, H
+            try:
+                g = EventSequenceToVoxelGrid_Pytorch(C, gpu=False, normalize=bool(norm), forkserver=False)(s)
+                out[f"{k}/norm{norm}"] = g.numpy()
+            except (IndexError, RuntimeError):
+                out[f"{k}/raises"] = np.array(True)
+    torch.set_num_threads(8)
+    return out
+
+
 def main():
     np.savez_compressed(os.path.join(HERE, "next_splat.npz"), **splat_cases())
     print("wrote next_splat.npz")
     np.savez_compressed(os.path.join(HERE, "next_flow.npz"), **flow_cases())
     print("wrote next_flow.npz")
+    np.savez_compressed(os.path.join(HERE, "next_voxel.npz"), **voxel_cases())
+    print("wrote next_voxel.npz")
 
 
 if __name__ == "__main__":

@@ -60,3 +60,24 @@ def coords_with_flow(seed: int, B: int, H: int, W: int, sigma: float) -> np.ndar
     if sigma == 0.0:
         return np.ascontiguousarray(grid)
     return np.ascontiguousarray(grid + normal(seed, (B, 2, H, W), sigma))
+
+
+def dsec_events(seed: int, n: int, H: int, W: int):
+    """Synthetic DSEC events as the loader hands them to VoxelGrid.convert (loader_dsec.py:245-257):
+    fp32 p in {0, 1}, t ascending from 0 (us), rectified x / y reaching slightly outside the image."""
+    t = np.sort(uniform(seed, (n,), 0.0, 1e5)).astype(np.float32)
+    t -= t[0]
+    x = uniform(seed + 1, (n,), -1.5, W + 0.5)
+    y = uniform(seed + 2, (n,), -1.5, H + 0.5)
+    p = (uniform(seed + 3, (n,)) < 0.5).astype(np.float32)
+    return p, t, x, y
+
+
+def mvsec_events(seed: int, n: int, H: int, W: int):
+    """Synthetic MVSEC event sequence features [n, 4] float64 (t ascending in s, integer x / y,
+    p in {0, 1}), the input of EventSequenceToVoxelGrid_Pytorch."""
+    t = np.sort(uniform(seed, (n,), 0.0, 1.0)).astype(np.float64) * 0.05 + 1400000000.0
+    x = np.floor(uniform(seed + 1, (n,), 0.0, W)).astype(np.float64)
+    y = np.floor(uniform(seed + 2, (n,), 0.0, H)).astype(np.float64)
+    p = (uniform(seed + 3, (n,)) < 0.5).astype(np.float64)
+    return np.ascontiguousarray(np.stack([t, x, y, p], 1))

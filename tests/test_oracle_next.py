@@ -64,3 +64,27 @@ def test_png16_codec_oracle_bit_exact(flowz):
     assert np.array_equal(valid, flowz["dec/valid"])
     assert np.array_equal(flow.astype(np.float64), flowz["dec/flow"])   # exact in float32
     assert bool(flowz["dec_bad/raises"]) and oracle.flow_16bit_to_float(flowz["dec_bad/png"])[2] == 1
+
+
+@pytest.fixture(scope="module")
+def voxz():
+    return np.load(os.path.join(GOLD, "next_voxel.npz"))
+
+
+def test_voxel_oracle_vs_reference(voxz):
+    """Accumulated grids bit-exact (serial fold); normalized within 2 ulp-ish (reduction order)."""
+    from voxel_cases import DSEC_VOXEL, MVSEC_VOXEL, dsec_case, mvsec_case
+    for k, (n, C, H, W, seed) in DSEC_VOXEL.items():
+        p, t, x, y = dsec_case(k, n, H, W, seed)
+        assert oracle.same_bits(oracle.voxel_dsec(p, t, x, y, C, H, W, False), voxz[f"{k}/norm0"]), k
+        got = oracle.voxel_dsec(p, t, x, y, C, H, W, True)
+        np.testing.assert_allclose(got, voxz[f"{k}/norm1"], rtol=1e-6, atol=1e-6, err_msg=k)
+    for k, (n, C, H, W, seed) in MVSEC_VOXEL.items():
+        ev = mvsec_case(k, n, H, W, seed)
+        g0, bad = oracle.voxel_mvsec(ev, C, H, W, False)
+        if f"{k}/raises" in voxz.files:
+            assert bad, k
+            continue
+        assert not bad and oracle.same_bits(g0, voxz[f"{k}/norm0"]), k
+        g1, _ = oracle.voxel_mvsec(ev, C, H, W, True)
+        np.testing.assert_allclose(g1, voxz[f"{k}/norm1"], rtol=1e-6, atol=1e-6, err_msg=k)

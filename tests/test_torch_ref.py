@@ -34,3 +34,18 @@ def test_torch_ref_splat_matches_reference():
     for k in sorted(f.split("/")[0] for f in z.files if f.startswith("fi_") and f.endswith("/flow")):
         got = torch_ref.forward_interpolate_pytorch(torch.from_numpy(z[f"{k}/flow"])).numpy()
         assert oracle.same_bits(got, z[f"{k}/out"]), k
+
+
+def test_torch_ref_voxel_matches_reference():
+    from voxel_cases import DSEC_VOXEL, dsec_case
+    import torch_ref
+    z = np.load(os.path.join(GOLDEN, "next_voxel.npz"))
+    torch.set_num_threads(1)
+    try:
+        for k, (n, C, H, W, seed) in DSEC_VOXEL.items():
+            ev = {c: torch.from_numpy(v) for c, v in zip("ptxy", dsec_case(k, n, H, W, seed))}
+            for norm in (0, 1):
+                got = torch_ref.voxel_grid_dsec(ev, C, H, W, bool(norm)).numpy()
+                assert oracle.same_bits(got, z[f"{k}/norm{norm}"]), (k, norm)
+    finally:
+        torch.set_num_threads(os.cpu_count() or 1)

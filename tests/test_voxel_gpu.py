@@ -1,0 +1,91 @@
+"""GPU parity of the event -> voxel grid (voxel.hip) through the C ABI: the
+accumulated grid bit-exact with the reference's serial fold (goldens, and the oracle at DSEC full
+resolution with 1M events); the normalized grid within NORM_TOL (reduction order only)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import prng
+from voxel_cases import DSEC_VOXEL, MVSEC_VOXEL, dsec_case, mvsec_case
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NORM_TOL = 1e-6   # rtol and atol on the normalized grid
+
+
+@pytest.fixture(scope="module")
+def ea():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    import eraft_amd
+    eraft_amd.lib()
+    return eraft_amd
+
+
+@pytest.fixture(scope="module")
+def voxz():
+    return np.load(os.path.join(GOLD, "next_voxel.npz"))
+
+
+class _Seq:
+    pass
+
+
+def _dsec(ea, p, t, x, y, C, H, W, norm):
+    ev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in zip("ptxy", (p, t, x, y))}
+    return ea.VoxelGrid((C, H, W), normalize=norm).convert(ev).cpu().numpy()
+
+
+def _mvsec(ea, ev, C, H, W, norm):
+    s = _Seq()
+    s.features, s.image_width, s.image_height = ev, W, H
+    return ea.EventSequenceToVoxelGrid_Pytorch(C, gpu=True, normalize=norm)(s).cpu().numpy()
+
+
+def test_voxel_dsec_goldens(ea, voxz):
+    for k, (n, C, H, W, seed) in DSEC_VOXEL.items():
+        p, t, x, y = dsec_case(k, n, H, W, seed)
+        assert oracle.same_bits(_dsec(ea, p, t, x, y, C, H, W, False), voxz[f"{k}/norm0"]), k
+        np.testing.assert_allclose(_dsec(ea, p, t, x, y, C, H, W, True), voxz[f"{k}/norm1"],
+                                   rtol=NORM_TOL, atol=NORM_TOL, err_msg=k)
+
+
+def test_voxel_mvsec_goldens(ea, voxz):
+    for k, (n, C, H, W, seed) in MVSEC_VOXEL.items():
+        ev = mvsec_case(k, n, H, W, seed)
+        if f"{k}/raises" in voxz.files:
+            with pytest.raises(IndexError):
+                _mvsec(ea, ev, C, H, W, True)
+            continue
+        assert oracle.same_bits(_mvsec(ea, ev, C, H, W, False), voxz[f"{k}/norm0"]), k
+        np.testing.assert_allclose(_mvsec(ea, ev, C, H, W, True), voxz[f"{k}/norm1"],
+                                   rtol=NORM_TOL, atol=NORM_TOL, err_msg=k)
+
+
+def test_voxel_dsec_full_res_vs_oracle(ea):
+    # DSEC 15 x 480 x 640 with 1M events: bit-exact accumulation, deterministic run to run
+    n, C, H, W = 1_000_000, 15, 480, 640
+    p, t, x, y = prng.dsec_events(700, n, H, W)
+    g = _dsec(ea, p, t, x, y, C, H, W, False)
+    assert oracle.same_bits(g, oracle.voxel_dsec(p, t, x, y, C, H, W, False))
+    g1 = _dsec(ea, p, t, x, y, C, H, W, True)
+    np.testing.assert_allclose(g1, oracle.voxel_dsec(p, t, x, y, C, H, W, True), rtol=NORM_TOL, atol=NORM_TOL)
+    assert np.array_equal(g1, _dsec(ea, p, t, x, y, C, H, W, True))
+
+
+def test_voxel_mvsec_full_res_vs_oracle(ea):
+    n, C, H, W = 300_000, 15, 260, 346
+    ev = prng.mvsec_events(710, n, H, W)
+    g = _mvsec(ea, ev, C, H, W, False)
+    ref, bad = oracle.voxel_mvsec(ev, C, H, W, False)
+    assert not bad and oracle.same_bits(g, ref)
+
+
+def test_voxel_rejects_cpu_events(ea):
+    p, t, x, y = prng.dsec_events(720, 10, 4, 4)
+    with pytest.raises(RuntimeError):
+        ea.VoxelGrid((2, 4, 4), True).convert({k: torch.from_numpy(v) for k, v in zip("ptxy", (p, t, x, y))})
