@@ -39,6 +39,8 @@ def gather_rows(slab, counts, group=None):
     Slabs are zero-padded to max(counts) rows so one fixed-size collective serves ragged splits.
     """
     world = dist.get_world_size(group)
+    if world == 1:
+        return slab.contiguous()
     maxr = max(counts)
     lead = slab.shape[:-2]
     W = slab.shape[-1]

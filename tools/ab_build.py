@@ -13,11 +13,11 @@ import eraft_amd  # noqa: E402
 
 VARIANTS = {
     "default": {},
-    "noband": {"ECORR_BUILD_NOBAND": "1"},
-    "kb32": {"ECORR_BUILD_KB32": "1"},
+    "nopipe": {"ECORR_BUILD_NOPIPE": "1"},
     "noepi": {"ECORR_BUILD_SKIP_EPILOGUE": "1"},
+    "nol0st": {"ECORR_BUILD_SKIP_EPILOGUE": "2"},
 }
-KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32", "ECORR_BUILD_NOBAND")
+KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32", "ECORR_BUILD_NOBAND", "ECORR_BUILD_NOPIPE")
 B = int(os.environ.get("AB_BATCH", "16"))
 H, W, D = 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)
@@ -34,7 +34,7 @@ with torch.no_grad():
             os.environ.update(env)
             blk = eraft_amd.CorrBlock(f1, f2)   # warm
             torch.cuda.synchronize()
-            if rnd == 0 and "noepi" not in name:   # every variant must produce a valid pyramid (pooling exact vs level 0)
+            if rnd == 0 and "noepi" not in name and "nol0" not in name:   # every variant must produce a valid pyramid (pooling exact vs level 0)
                 blk._levels_cache = None
                 lv0, lv1 = blk.corr_pyramid[0][:64, 0], blk.corr_pyramid[1][:64, 0]
                 p = (((lv0[:, 0::2, 0::2] + lv0[:, 0::2, 1::2]) + lv0[:, 1::2, 0::2]) + lv0[:, 1::2, 1::2]) * 0.25
