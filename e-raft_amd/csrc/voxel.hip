@@ -10,18 +10,24 @@
 //   prep    per event: the reference's fp32/fp64 arithmetic up to the base cell key (the cell its
 //           pass-0 corner lands in; DSEC keys live on a grid extended by one cell on the low side
 //           because x0 = -1 still reaches x = 0) and the per-event factors the weights need;
-//   sort    stable LSD radix sort of (key, event index) pairs (rocPRIM onesweep) -- each base
-//           cell's events end up contiguous and in event order;
-//   bounds  start/end of every base cell's run (one pass over the sorted keys, no atomics);
+//   bucket  counting sort by key: per-key counts (integer atomics, in prep), exclusive scan
+//           (rocPRIM), events dropped into their key's run (integer atomics pick the slot);
+//   order   per key, its run insertion-sorted by event index (runs are short and the atomics
+//           hand out slots nearly in event order, so this is ~linear) and the events' weight
+//           factors gathered once into run order (one float4 each);
 //   gather  per target cell, the runs of the base cells its 8 (DSEC) / 2 (MVSEC) passes read, in
-//           pass order, each in event order: the reference's fold, bit for bit;
-//   normalize  deterministic block reductions (count, double sum -> mean; double sum of squared
-//           deviations -> unbiased std), then (v - mean) / std on the nonzero cells.  ATen reduces
-//           in its own order, so normalized values agree within an ulp or two.
-// HBM-bound with random event access; every phase is a full-chip launch.
+//           pass order, each in event order: the reference's fold, bit for bit.  Neighbouring
+//           cells read neighbouring runs, so the payload reads are near-contiguous.  With
+//           normalize, each block also folds its nonzero cells into (count, mean, M2) (Chan's
+//           pairwise combination, double, fixed tree order);
+//   finalize one block combines the block partials in a fixed order -> mean, unbiased std;
+//   apply   (v - mean) / std on the nonzero cells.  ATen reduces in its own order, so normalized
+//           values agree within an ulp or two.
+// Memory-bound with random event access; every phase is a full-chip launch.
+#include <algorithm>
 #include <cstring>   // rocprim's texture_cache_iterator uses memset without including it
 
-#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
@@ -50,10 +56,13 @@ struct VoxelArgs {
     int64_t n;
     int C, H, W;
     uint32_t K;           // key range; key K = no contribution
-    uint32_t *key_in, *key_out;
-    int *idx_in, *idx_out;
+    uint32_t* key;        // per event: base-cell key (K = none)
+    uint32_t* cnt;        // per key: event count (zeroed), then
+    uint32_t* off;        // per key: exclusive offset, after the fill the run end (start = off[k-1])
+    int* slot;            // run order: event index
     float *fa, *fb;       // DSEC: t_norm, value; MVSEC: left, right (0 when the right pass is masked)
-    uint32_t *run_start, *run_end;
+    float4* payload;      // sorted order: DSEC (x, y, t_norm, value); MVSEC (left, right, -, -)
+    double* part;         // per gather block: count, mean, M2 of its nonzero cells
     float* voxel;
     int* bad;             // MVSEC: an index outside the grid (the reference raises)
 };
@@ -68,8 +77,9 @@ __global__ __launch_bounds__(NTV) void prep_dsec(VoxelArgs A) {
     // base cell on the grid extended by one on the low side: corners x0 .. x0+1 touch [0, W) iff
     // x0 in [-1, W-1]
     const bool in = x0 >= -1 && x0 < A.W && y0 >= -1 && y0 < A.H && ti >= -1 && ti < A.C;
-    A.key_in[e] = in ? (uint32_t)(((int64_t)(ti + 1) * (A.H + 1) + (y0 + 1)) * (A.W + 1) + (x0 + 1)) : A.K;
-    A.idx_in[e] = (int)e;
+    const uint32_t k = in ? (uint32_t)(((int64_t)(ti + 1) * (A.H + 1) + (y0 + 1)) * (A.W + 1) + (x0 + 1)) : A.K;
+    A.key[e] = k;
+    if (in) atomicAdd(&A.cnt[k], 1u);
     A.fa[e] = tn;
     A.fb[e] = __fsub_rn(__fmul_rn(2.0f, A.p[e]), 1.0f);   // :41 value = 2*p - 1
 }
@@ -94,129 +104,138 @@ __global__ __launch_bounds__(NTV) void prep_mvsec(VoxelArgs A) {
     const long long idx = xs + ys * A.W + x86_i64(tis) * HW;   // :108-110
     if ((vl && (idx < 0 || idx >= CHW)) || (vr && (idx + HW < 0 || idx + HW >= CHW))) atomicOr(A.bad, 1);
     const bool ok = vl && idx >= 0 && idx < CHW;
-    A.key_in[e] = ok ? (uint32_t)idx : A.K;
-    A.idx_in[e] = (int)e;
+    A.key[e] = ok ? (uint32_t)idx : A.K;
+    if (ok) atomicAdd(&A.cnt[idx], 1u);
     A.fa[e] = __fmul_rn(pol, __fsub_rn(1.0f, dts));           // :96 vals_left
     A.fb[e] = vr ? __fmul_rn(pol, dts) : 0.0f;                 // :97 vals_right (+0: a no-op add)
 }
 
-// start/end of each key's run in the sorted keys (buffers zeroed: empty runs read [0, 0)).
-__global__ __launch_bounds__(NTV) void run_bounds(VoxelArgs A) {
-    const int64_t i = blockIdx.x * (int64_t)NTV + threadIdx.x;
-    if (i >= A.n) return;
-    const uint32_t k = A.key_out[i];
-    if (k >= A.K) return;
-    if (i == 0 || A.key_out[i - 1] != k) A.run_start[k] = (uint32_t)i;
-    if (i == A.n - 1 || A.key_out[i + 1] != k) A.run_end[k] = (uint32_t)(i + 1);
+// Drop every event into its key's run; off[k] walks from the run start to the next run's start.
+__global__ __launch_bounds__(NTV) void fill_runs(VoxelArgs A) {
+    const int64_t e = blockIdx.x * (int64_t)NTV + threadIdx.x;
+    if (e >= A.n) return;
+    const uint32_t k = A.key[e];
+    if (k < A.K) A.slot[atomicAdd(&A.off[k], 1u)] = (int)e;
 }
 
-__global__ __launch_bounds__(NTV) void gather_dsec(VoxelArgs A) {
-    const int64_t HW = (int64_t)A.H * A.W;
-    const int64_t cell = blockIdx.x * (int64_t)NTV + threadIdx.x;
-    if (cell >= HW * A.C) return;
-    const int tc = (int)(cell / HW), rem = (int)(cell - tc * HW), yc = rem / A.W, xc = rem - yc * A.W;
-    const float fx = (float)xc, fy = (float)yc, ft = (float)tc;
-    float acc = 0.0f;
-    // dsec_utils.py:43-45 pass order: xlim outer, ylim, tlim inner
+__device__ __forceinline__ uint2 run_of(const VoxelArgs& A, int64_t k) {
+    return make_uint2(k > 0 ? A.off[k - 1] : 0u, A.off[k]);
+}
+
+// Per key: order its run by event index, then gather the events' weight factors into run order.
+template <bool DSEC>
+__global__ __launch_bounds__(NTV) void order_runs(VoxelArgs A) {
+    const int64_t k = blockIdx.x * (int64_t)NTV + threadIdx.x;
+    if (k >= A.K) return;
+    const uint2 r = run_of(A, k);
+    for (uint32_t i = r.x + 1; i < r.y; ++i) {
+        const int v = A.slot[i];
+        uint32_t j = i;
+        while (j > r.x && A.slot[j - 1] > v) { A.slot[j] = A.slot[j - 1]; --j; }
+        A.slot[j] = v;
+    }
+    for (uint32_t i = r.x; i < r.y; ++i) {
+        const int e = A.slot[i];
+        A.payload[i] = DSEC ? make_float4(A.x[e], A.y[e], A.fa[e], A.fb[e]) : make_float4(A.fa[e], A.fb[e], 0.0f, 0.0f);
+    }
+}
+
+// (count, mean, M2) of a set of values; Chan et al.'s pairwise combination, in double.
+struct Moments {
+    double n, mean, m2;
+};
+__device__ __forceinline__ Moments combine(Moments a, Moments b) {
+    const double n = a.n + b.n;
+    if (n == 0.0) return a;
+    const double d = b.mean - a.mean;
+    return {n, a.mean + d * (b.n / n), a.m2 + b.m2 + d * d * (a.n * b.n / n)};
+}
+
+// Fixed-order tree over the block (deterministic); result valid in thread 0.
+__device__ __forceinline__ Moments block_moments(Moments m, double* sh) {
+    const int tid = threadIdx.x;
+    sh[3 * tid] = m.n; sh[3 * tid + 1] = m.mean; sh[3 * tid + 2] = m.m2;
+    __syncthreads();
+    for (int s = NTV / 2; s > 0; s >>= 1) {
+        if (tid < s) {
+            const Moments r = combine({sh[3 * tid], sh[3 * tid + 1], sh[3 * tid + 2]},
+                                      {sh[3 * (tid + s)], sh[3 * (tid + s) + 1], sh[3 * (tid + s) + 2]});
+            sh[3 * tid] = r.n; sh[3 * tid + 1] = r.mean; sh[3 * tid + 2] = r.m2;
+        }
+        __syncthreads();
+    }
+    return {sh[0], sh[1], sh[2]};
+}
+
+template <bool DSEC>
+__global__ __launch_bounds__(NTV) void gather(VoxelArgs A, int normalize) {
+    __shared__ double sh[3 * NTV];
+    const int64_t HW = (int64_t)A.H * A.W, cells = HW * A.C;
+    Moments mom{0.0, 0.0, 0.0};   // this thread's nonzero cells, folded in cell order
+    for (int64_t cell = blockIdx.x * (int64_t)NTV + threadIdx.x; cell < cells; cell += (int64_t)gridDim.x * NTV) {
+        float acc = 0.0f;
+        if (DSEC) {
+            const int tc = (int)(cell / HW), rem = (int)(cell - tc * HW), yc = rem / A.W, xc = rem - yc * A.W;
+            const float fx = (float)xc, fy = (float)yc, ft = (float)tc;
+            // dsec_utils.py:43-45 pass order: xlim outer, ylim, tlim inner
 #pragma unroll
-    for (int pass = 0; pass < 8; ++pass) {
-        const int a = pass >> 2, b = (pass >> 1) & 1, c = pass & 1;
-        const int64_t k = ((int64_t)(tc - c + 1) * (A.H + 1) + (yc - b + 1)) * (A.W + 1) + (xc - a + 1);
-        const uint32_t lo = A.run_start[k], hi = A.run_end[k];
-        for (uint32_t j = lo; j < hi; ++j) {
-            const int e = A.idx_out[j];
-            // :48 value * (1 - |xlim - x|) * (1 - |ylim - y|) * (1 - |tlim - t_norm|), left to right
-            float wgt = __fmul_rn(A.fb[e], __fsub_rn(1.0f, fabsf(__fsub_rn(fx, A.x[e]))));
-            wgt = __fmul_rn(wgt, __fsub_rn(1.0f, fabsf(__fsub_rn(fy, A.y[e]))));
-            wgt = __fmul_rn(wgt, __fsub_rn(1.0f, fabsf(__fsub_rn(ft, A.fa[e]))));
-            acc = __fadd_rn(acc, wgt);
+            for (int pass = 0; pass < 8; ++pass) {
+                const int a = pass >> 2, b = (pass >> 1) & 1, c = pass & 1;
+                const int64_t k = ((int64_t)(tc - c + 1) * (A.H + 1) + (yc - b + 1)) * (A.W + 1) + (xc - a + 1);
+                const uint2 run = run_of(A, k);
+                for (uint32_t j = run.x; j < run.y; ++j) {
+                    const float4 ev = A.payload[j];
+                    // :48 value * (1 - |xlim - x|) * (1 - |ylim - y|) * (1 - |tlim - t_norm|), left to right
+                    float wgt = __fmul_rn(ev.w, __fsub_rn(1.0f, fabsf(__fsub_rn(fx, ev.x))));
+                    wgt = __fmul_rn(wgt, __fsub_rn(1.0f, fabsf(__fsub_rn(fy, ev.y))));
+                    wgt = __fmul_rn(wgt, __fsub_rn(1.0f, fabsf(__fsub_rn(ft, ev.z))));
+                    acc = __fadd_rn(acc, wgt);
+                }
+            }
+        } else {
+            // transformers.py:103-113: all left contributions, then all right ones (+W*H)
+            const uint2 rl = run_of(A, cell);
+            for (uint32_t j = rl.x; j < rl.y; ++j) acc = __fadd_rn(acc, A.payload[j].x);
+            if (cell >= HW) {
+                const uint2 rr = run_of(A, cell - HW);
+                for (uint32_t j = rr.x; j < rr.y; ++j) acc = __fadd_rn(acc, A.payload[j].y);
+            }
+        }
+        A.voxel[cell] = acc;
+        if (normalize && acc != 0.0f) mom = combine(mom, {1.0, (double)acc, 0.0});
+    }
+    if (normalize) {   // uniform over the grid
+        const Moments m = block_moments(mom, sh);
+        if (threadIdx.x == 0) {
+            A.part[3 * blockIdx.x] = m.n;
+            A.part[3 * blockIdx.x + 1] = m.mean;
+            A.part[3 * blockIdx.x + 2] = m.m2;
         }
     }
-    A.voxel[cell] = acc;
-}
-
-__global__ __launch_bounds__(NTV) void gather_mvsec(VoxelArgs A) {
-    const int64_t HW = (int64_t)A.H * A.W;
-    const int64_t cell = blockIdx.x * (int64_t)NTV + threadIdx.x;
-    if (cell >= HW * A.C) return;
-    float acc = 0.0f;
-    for (uint32_t j = A.run_start[cell], hi = A.run_end[cell]; j < hi; ++j) acc = __fadd_rn(acc, A.fa[A.idx_out[j]]);
-    if (cell >= HW)
-        for (uint32_t j = A.run_start[cell - HW], hi = A.run_end[cell - HW]; j < hi; ++j)
-            acc = __fadd_rn(acc, A.fb[A.idx_out[j]]);
-    A.voxel[cell] = acc;
 }
 
 // ---- normalization (dsec_utils.py:55-62, transformers.py:117-124)
 struct NormState {
-    double mean64;
     float mean, stdv;
-    long long count;
+    int any;
 };
 
-template <typename T>
-__device__ __forceinline__ T block_sum(T v, T* sh) {
-    const int tid = threadIdx.x;
-    sh[tid] = v;
-    __syncthreads();
-    for (int s = NTV / 2; s > 0; s >>= 1) {
-        if (tid < s) sh[tid] += sh[tid + s];
-        __syncthreads();
-    }
-    const T r = sh[0];
-    __syncthreads();
-    return r;
-}
-
-// pass 0: count + sum of the nonzero cells; pass 1: sum of squared deviations from the mean.
-// Fixed partition and tree order -> deterministic.
-__global__ __launch_bounds__(NTV) void norm_partials(const float* __restrict__ g, int64_t n, int pass,
-                                                     const NormState* st, double* part, long long* cpart) {
-    __shared__ double shd[NTV];
-    __shared__ long long shc[NTV];
-    const double m = pass ? st->mean64 : 0.0;
-    double s = 0.0;
-    long long c = 0;
-    for (int64_t i = blockIdx.x * (int64_t)NTV + threadIdx.x; i < n; i += (int64_t)gridDim.x * NTV) {
-        const float v = g[i];
-        if (v != 0.0f) {
-            const double d = (double)v - m;
-            s += pass ? d * d : (double)v;
-            ++c;
-        }
-    }
-    s = block_sum(s, shd);
-    c = block_sum(c, shc);
+// One block: thread t folds partials t, t + NTV, ... in order, then the fixed tree.
+__global__ __launch_bounds__(NTV) void norm_finalize(const double* part, int nparts, NormState* st) {
+    __shared__ double sh[3 * NTV];
+    Moments m{0.0, 0.0, 0.0};
+    for (int i = threadIdx.x; i < nparts; i += NTV) m = combine(m, {part[3 * i], part[3 * i + 1], part[3 * i + 2]});
+    m = block_moments(m, sh);
     if (threadIdx.x == 0) {
-        part[blockIdx.x] = s;
-        cpart[blockIdx.x] = c;
-    }
-}
-
-__global__ __launch_bounds__(NTV) void norm_finalize(int pass, const double* part, const long long* cpart,
-                                                     NormState* st) {
-    __shared__ double shd[NTV];
-    __shared__ long long shc[NTV];
-    double s = 0.0;
-    long long c = 0;
-    for (int i = threadIdx.x; i < kRedBlocks; i += NTV) {
-        s += part[i];
-        c += cpart[i];
-    }
-    s = block_sum(s, shd);
-    c = block_sum(c, shc);
-    if (threadIdx.x == 0) {
-        if (pass == 0) {
-            st->count = c;
-            st->mean64 = c > 0 ? s / (double)c : 0.0;
-            st->mean = (float)st->mean64;
-        } else {
-            st->stdv = c > 1 ? (float)sqrt(s / (double)(c - 1)) : __int_as_float(0x7fc00000);   // NaN for 1 cell
-        }
+        st->any = m.n > 0.0;
+        st->mean = (float)m.mean;
+        // unbiased std; one nonzero cell gives NaN like torch.std, and then v - mean
+        st->stdv = m.n > 1.0 ? (float)sqrt(m.m2 / (m.n - 1.0)) : __int_as_float(0x7fc00000);
     }
 }
 
 __global__ __launch_bounds__(NTV) void norm_apply(float* __restrict__ g, int64_t n, const NormState* st) {
+    if (!st->any) return;
     const float mean = st->mean, sd = st->stdv;
     for (int64_t i = blockIdx.x * (int64_t)NTV + threadIdx.x; i < n; i += (int64_t)gridDim.x * NTV) {
         const float v = g[i];
@@ -230,36 +249,31 @@ inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // Workspace carve-up (every piece 256-byte aligned).
 struct VoxelWs {
-    size_t key_in, key_out, idx_in, idx_out, fa, fb, run_start, run_end, norm, part, cpart, sort_tmp, total;
-    size_t sort_bytes;
+    size_t key, cnt, off, slot, fa, fb, payload, norm, part, scan_tmp, total;
+    size_t scan_bytes;
 };
 
-unsigned key_bits(uint32_t K) {
-    unsigned b = 1;
-    while (b < 32 && ((uint64_t)1 << b) <= K) ++b;
-    return b;
-}
+constexpr int kGatherBlocks = 2048;   // grid-stride gather: this many normalization partials
 
-int plan(int64_t n, uint32_t K, VoxelWs* w) {
-    size_t sort_bytes = 0;
-    const hipError_t e = rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                   (int*)nullptr, (int*)nullptr, (size_t)n, 0, key_bits(K));
+int plan(int64_t n, uint32_t K, int64_t cells, VoxelWs* w) {
+    size_t scan_bytes = 0;
+    const hipError_t e = rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
+                                                 (size_t)K, rocprim::plus<uint32_t>());
     if (e != hipSuccess) return ECORR_EHIP - (int)e;
+    (void)cells;
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t at = o; o += align256(bytes); return at; };
-    w->key_in = take(4 * (size_t)n);
-    w->key_out = take(4 * (size_t)n);
-    w->idx_in = take(4 * (size_t)n);
-    w->idx_out = take(4 * (size_t)n);
+    w->key = take(4 * (size_t)n);
+    w->cnt = take(4 * (size_t)K);
+    w->off = take(4 * (size_t)K);
+    w->slot = take(4 * (size_t)n);
     w->fa = take(4 * (size_t)n);
     w->fb = take(4 * (size_t)n);
-    w->run_start = take(4 * (size_t)K);
-    w->run_end = take(4 * (size_t)K);
+    w->payload = take(16 * (size_t)n);
     w->norm = take(sizeof(NormState));
-    w->part = take(8 * (size_t)kRedBlocks);
-    w->cpart = take(8 * (size_t)kRedBlocks);
-    w->sort_bytes = sort_bytes;
-    w->sort_tmp = take(sort_bytes);
+    w->part = take(3 * 8 * (size_t)kGatherBlocks);
+    w->scan_bytes = scan_bytes;
+    w->scan_tmp = take(scan_bytes);
     w->total = o;
     return ECORR_OK;
 }
@@ -277,7 +291,7 @@ uint32_t voxel_key_range(bool dsec, int C, int H, int W) {
 
 int voxel_workspace_bytes(bool dsec, int64_t n, int C, int H, int W, int64_t* bytes) {
     VoxelWs w;
-    const int st = plan(n, voxel_key_range(dsec, C, H, W), &w);
+    const int st = plan(n, voxel_key_range(dsec, C, H, W), (int64_t)C * H * W, &w);
     if (st == ECORR_OK) *bytes = (int64_t)w.total;
     return st;
 }
@@ -290,44 +304,40 @@ int launch_voxel(bool dsec, const float* p, const float* t, const float* x, cons
     A.n = n; A.C = C; A.H = H; A.W = W;
     A.K = voxel_key_range(dsec, C, H, W);
     VoxelWs w;
-    int st = plan(n, A.K, &w);
+    const int64_t cells = (int64_t)C * H * W;
+    int st = plan(n, A.K, cells, &w);
     if (st != ECORR_OK) return st;
     char* base = (char*)workspace;
-    A.key_in = (uint32_t*)(base + w.key_in);
-    A.key_out = (uint32_t*)(base + w.key_out);
-    A.idx_in = (int*)(base + w.idx_in);
-    A.idx_out = (int*)(base + w.idx_out);
+    A.key = (uint32_t*)(base + w.key);
+    A.cnt = (uint32_t*)(base + w.cnt);
+    A.off = (uint32_t*)(base + w.off);
+    A.slot = (int*)(base + w.slot);
     A.fa = (float*)(base + w.fa);
     A.fb = (float*)(base + w.fb);
-    A.run_start = (uint32_t*)(base + w.run_start);
-    A.run_end = (uint32_t*)(base + w.run_end);
+    A.payload = (float4*)(base + w.payload);
+    A.part = (double*)(base + w.part);
     A.voxel = voxel;
     A.bad = bad;
     NormState* ns = (NormState*)(base + w.norm);
 
+    hipError_t e = hipMemsetAsync(A.cnt, 0, 4 * (size_t)A.K, stream);
+    if (e != hipSuccess) return ECORR_EHIP - (int)e;
     if (dsec) hipLaunchKernelGGL(prep_dsec, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
     else hipLaunchKernelGGL(prep_mvsec, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
     if ((st = hip_status()) != ECORR_OK) return st;
-    size_t sort_bytes = w.sort_bytes;
-    hipError_t e = rocprim::radix_sort_pairs(base + w.sort_tmp, sort_bytes, A.key_in, A.key_out, A.idx_in, A.idx_out,
-                                             (size_t)n, 0, key_bits(A.K), stream);
+    size_t scan_bytes = w.scan_bytes;
+    e = rocprim::exclusive_scan(base + w.scan_tmp, scan_bytes, A.cnt, A.off, 0u, (size_t)A.K,
+                                rocprim::plus<uint32_t>(), stream);
     if (e != hipSuccess) return ECORR_EHIP - (int)e;
-    e = hipMemsetAsync(A.run_start, 0, 4 * (size_t)A.K, stream);
-    if (e == hipSuccess) e = hipMemsetAsync(A.run_end, 0, 4 * (size_t)A.K, stream);
-    if (e != hipSuccess) return ECORR_EHIP - (int)e;
-    hipLaunchKernelGGL(run_bounds, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
-    const int64_t cells = (int64_t)C * H * W;
-    if (dsec) hipLaunchKernelGGL(gather_dsec, dim3(blocks_for(cells)), dim3(NTV), 0, stream, A);
-    else hipLaunchKernelGGL(gather_mvsec, dim3(blocks_for(cells)), dim3(NTV), 0, stream, A);
+    hipLaunchKernelGGL(fill_runs, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
+    if (dsec) hipLaunchKernelGGL(order_runs<true>, dim3(blocks_for(A.K)), dim3(NTV), 0, stream, A);
+    else hipLaunchKernelGGL(order_runs<false>, dim3(blocks_for(A.K)), dim3(NTV), 0, stream, A);
+    const unsigned gblocks = (unsigned)std::min<int64_t>(kGatherBlocks, blocks_for(cells));
+    if (dsec) hipLaunchKernelGGL(gather<true>, dim3(gblocks), dim3(NTV), 0, stream, A, normalize);
+    else hipLaunchKernelGGL(gather<false>, dim3(gblocks), dim3(NTV), 0, stream, A, normalize);
     if ((st = hip_status()) != ECORR_OK) return st;
     if (normalize) {
-        double* part = (double*)(base + w.part);
-        long long* cpart = (long long*)(base + w.cpart);
-        for (int pass = 0; pass < 2; ++pass) {
-            hipLaunchKernelGGL(norm_partials, dim3(kRedBlocks), dim3(NTV), 0, stream, voxel, cells, pass, ns, part,
-                               cpart);
-            hipLaunchKernelGGL(norm_finalize, dim3(1), dim3(NTV), 0, stream, pass, part, cpart, ns);
-        }
+        hipLaunchKernelGGL(norm_finalize, dim3(1), dim3(NTV), 0, stream, A.part, (int)gblocks, ns);
         hipLaunchKernelGGL(norm_apply, dim3(kRedBlocks), dim3(NTV), 0, stream, voxel, cells, ns);
     }
     return hip_status();
