@@ -113,9 +113,19 @@ def cpu_baseline(B, D, H, W, iters, seconds):
         el = time.perf_counter() - t0
         if el >= seconds or pairs >= 64:
             break
+    # the reference's own setting: main.py:2-5 pins torch to one thread
+    torch.set_num_threads(1)
+    blk1 = TorchCpuCorrBlock(f1[:1], f2[:1])
+    t1 = time.perf_counter()
+    for c in coords:
+        blk1(c[:1])
+    one = time.perf_counter() - t1
+    torch.set_num_threads(cores)
     return {"value": pairs / el, "unit": "pairs/s", "cores": cores, "kind": "port",
             "sample": f"{pairs} pairs ({nb} per step, fmap {D}x{H}x{W}, build + {iters} lookups) in "
-                      f"{el:.1f} s; torch {torch.__version__} CPU ops = the reference's ATen ops"}
+                      f"{el:.1f} s; torch {torch.__version__} CPU ops = the reference's ATen ops",
+            "one_core": {"value": round(1.0 / one, 3), "unit": "pairs/s", "cores": 1,
+                         "sample": "1 pair, build + 12 lookups, torch.set_num_threads(1) as main.py:2-5"}}
 
 
 def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
