@@ -318,7 +318,7 @@ __device__ __forceinline__ void epilogue_band(const BuildParams& P, const TileCo
 // KB = K chunk depth; HALF = C tile handled in two 64-query halves.  KB = 16 + HALF needs 34 KB of
 // LDS and <= 168 VGPRs, so 3 blocks (3 waves per SIMD) share a CU; KB = 32 uses 67.5 KB (2 blocks).
 // (A/B: v_mfma_f32_16x16x4_f32 tiles, bitwise the same result, ran 1% slower than 32x32x2.)
-template <bool VEC, int KB, bool HALF, bool NTS, bool PIPE = true>
+template <bool VEC, int KB, bool HALF, bool NTS>
 __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) {
     constexpr int MR = HALF ? BM / 2 : BM;
     constexpr int AS = BM, BSS = BN;   // LDS row strides
@@ -402,34 +402,15 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
         if (kc + 1 < nk) load_chunk((kc + 1) * KB);
         const float* as = As + buf * KB * AS + wm * 64 + acol;
         const float* bs = Bs + buf * KB * BSS + wn * 64 + acol;
-        if (PIPE) {   // fragments of k-step kk+2 are read while the MFMAs of step kk run (the
-                      // compiler otherwise waits on each step's LDS reads right before its MFMAs)
-            float a0 = as[arow * AS], a1 = as[arow * AS + 32], b0 = bs[arow * BSS], b1 = bs[arow * BSS + 32];
 #pragma unroll
-            for (int kk = 0; kk < KB; kk += 2) {
-                float na0 = 0.f, na1 = 0.f, nb0 = 0.f, nb1 = 0.f;
-                if (kk + 2 < KB) {
-                    const int ro = kk + 2 + arow;
-                    na0 = as[ro * AS]; na1 = as[ro * AS + 32];
-                    nb0 = bs[ro * BSS]; nb1 = bs[ro * BSS + 32];
-                }
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-                a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
-            }
-        } else {
-#pragma unroll
-            for (int kk = 0; kk < KB; kk += 2) {
-                const int ro = kk + arow;
-                const float a0 = as[ro * AS], a1 = as[ro * AS + 32];
-                const float b0 = bs[ro * BSS], b1 = bs[ro * BSS + 32];
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-            }
+        for (int kk = 0; kk < KB; kk += 2) {
+            const int ro = kk + arow;
+            const float a0 = as[ro * AS], a1 = as[ro * AS + 32];
+            const float b0 = bs[ro * BSS], b1 = bs[ro * BSS + 32];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
         }
         if (kc + 1 < nk) store_chunk(buf ^ 1);
         __syncthreads();
@@ -522,9 +503,6 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
     const dim3 grid((unsigned)ntiles), block(NT);
     if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true>), grid, block, 0, stream, P);
     else if (kb32) hipLaunchKernelGGL((build_kernel<true, 32, false, true>), grid, block, 0, stream, P);
-    // dev knob (tools/ab_build.py): ECORR_BUILD_NOPIPE=1 reads each k-step's fragments right before
-    // its MFMAs instead of one step ahead (A/B: the prefetch is 1-2.5% faster)
-    else if (getenv("ECORR_BUILD_NOPIPE")) hipLaunchKernelGGL((build_kernel<true, 16, true, true, false>), grid, block, 0, stream, P);
     else hipLaunchKernelGGL((build_kernel<true, 16, true, true>), grid, block, 0, stream, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ECORR_EHIP - (int)e;

@@ -27,8 +27,11 @@ with torch.no_grad():
     algo = B * H * W * 2904
     times = {k: [] for k in VARIANTS}
     ref = None
-    for rnd in range(5):
-        for name, env in VARIANTS.items():
+    names = list(VARIANTS)
+    for rnd in range(6):
+        # rotate the order every round: the first variant of a round runs measurably slower
+        for name in names[rnd % len(names):] + names[:rnd % len(names)]:
+            env = VARIANTS[name]
             for k in KNOBS:
                 os.environ.pop(k, None)
             os.environ.update(env)
