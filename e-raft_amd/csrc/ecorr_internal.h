@@ -51,6 +51,8 @@ struct LookupParams {
     int lh[ECORR_MAX_LEVELS], lw[ECORR_MAX_LEVELS];
     int lntx[ECORR_MAX_LEVELS];      // tiles per tile row (0 = compact row-major)
     int lsz[ECORR_MAX_LEVELS];       // floats per query image
+    int dev_skip_mask;               // A/B ablation only (ECORR_LOOKUP_SKIP): levels whose window
+                                     // loads are dropped (output invalid)
 };
 
 int launch_lookup(const LookupParams& P, int B, hipStream_t stream);

@@ -114,14 +114,24 @@ __device__ __forceinline__ void stage_level(WindowStage<R, QB>& st, const Lookup
         const int x = st.org[gq][0] + rx, y0 = st.org[gq][1], info = st.org[gq][2];
         const int ny = (info >> 16) & 0xff;
         // only the needed corner rectangle touches memory; the slack row/column reads 0 for free
-        const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) && (unsigned)x < (unsigned)w;
-        const int base = (int)(gq * hw);
+        const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) && (unsigned)x < (unsigned)w &&
+                           !((P.dev_skip_mask >> lv) & 1);
         dst[c] = live ? gq * SP + rx : -1;
+        // rows ry in [rlo, rhi) are needed and inside the image; the column's byte offset walks
+        // down the rows incrementally (tiled: +8 floats inside a tile, + one tile row minus 24 from
+        // in-tile row 3; compact: +w) instead of re-deriving level_off per row
+        const int rlo = max(0, -y0), rhi = colin ? max(rlo, min(ny, h - y0)) : rlo;   // rhi >= rlo
+        const bool tiled = ntx > 0;
+        const int step_in = tiled ? 32 : 4 * w, step_wrap = tiled ? 128 * ntx - 96 : 4 * w;
+        int off = (int)(gq * hw) * 4 + (tiled ? ((((y0 >> 2) * ntx + (x >> 3)) << 5) + ((y0 & 3) << 3) + (x & 7)) * 4
+                                             : (y0 * w + x) * 4);
+        int ym = y0 & 3;
 #pragma unroll
         for (int ry = 0; ry < S; ++ry) {
-            const int y = y0 + ry;
-            const int off = (colin && ry < ny && (unsigned)y < (unsigned)h) ? (base + level_off(y, x, ntx, w)) * 4 : OOB;
-            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
+            const bool need = (unsigned)(ry - rlo) < (unsigned)(rhi - rlo);
+            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));
+            off += ym == 3 ? step_wrap : step_in;
+            ym = (ym + 1) & 3;
         }
     }
 #pragma unroll
