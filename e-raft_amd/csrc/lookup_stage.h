@@ -74,11 +74,11 @@ __device__ __forceinline__ void stage_level(WindowStage<R, QB>& st, const Lookup
         if (valid) {
             const float x0 = st.fx[g][0], y0 = st.fy[g][0];
             bool ok = fabsf(x0) < 1.0e7f && fabsf(y0) < 1.0e7f;  // false for NaN / inf / huge
-#pragma unroll
-            for (int o = 0; o < K; ++o) {
-                const float dx = st.fx[g][o] - x0, dy = st.fy[g][o] - y0;  // exact: integers < 2^24
-                ok &= (dx >= 0.0f) & (dx <= (float)(S - 2)) & (dy >= 0.0f) & (dy <= (float)(S - 2));
-            }
+            // every step of the chain (exact-or-rounded add of the offset, the normalize /
+            // unnormalize roundings by positive factors, floor) is monotone, so the floors are
+            // non-decreasing in the offset and the end points bound the whole window
+            const float dx = st.fx[g][K - 1] - x0, dy = st.fy[g][K - 1] - y0;   // exact: integers < 2^24
+            ok &= (dx >= 0.0f) & (dx <= (float)(S - 2)) & (dy >= 0.0f) & (dy <= (float)(S - 2));
             md = ok ? 0 : 1;
             X0 = ok ? (int)x0 : 0;
             Y0 = ok ? (int)y0 : 0;

@@ -12,8 +12,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import eraft_amd  # noqa: E402
 
-VARIANTS = {"cols3": {}, "staged4": {"ECORR_LOOKUP_V": "4"},
-            "cols3_skipall": {"ECORR_LOOKUP_SKIP": "15"}, "staged4_skipall": {"ECORR_LOOKUP_V": "4", "ECORR_LOOKUP_SKIP": "15"}}
+VARIANTS = {"cols3": {}, "staged4": {"ECORR_LOOKUP_V": "4"}, "cols3_skipall": {"ECORR_LOOKUP_SKIP": "15"}}
 KNOBS = ("ECORR_LOOKUP_QB", "ECORR_LOOKUP_V", "ECORR_LOOKUP_SKIP")
 B, H, W, D = int(os.environ.get("AB_BATCH", "16")), 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)
