@@ -62,8 +62,19 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
     for (int lv = 0; lv < (dev_phase == 2 ? 0 : P.levels); ++lv) {
         stage_level<R, QBM, NTM>(u.st, P, lv, b, q0, tid);
         const int md = u.st.org[g][2] & 0xff;
-        for (int k = part; k < KK; k += NTM / QBM)
-            T[lv * KK + k][g] = md == 2 ? 0.0f : sample_level<R, QBM>(u.st, P, lv, b, q0, g, k, md);
+        if (md == 0) {   // staged window: origin hoisted, no mode test per sample
+            constexpr int K = WS::K, S = WS::S;
+            const int o0 = u.st.org[g][0], o1 = u.st.org[g][1];
+            const float* wq = u.st.win + g * WS::SP;
+            for (int k = part; k < KK; k += NTM / QBM) {
+                const int a = k / K, bb = k - a * K;
+                const float* c = wq + ((int)u.st.fy[g][bb] - o1) * S + ((int)u.st.fx[g][a] - o0);
+                T[lv * KK + k][g] = blend(c[0], c[1], c[S], c[S + 1], u.st.wx[g][a], u.st.wy[g][bb]);
+            }
+        } else {
+            for (int k = part; k < KK; k += NTM / QBM)
+                T[lv * KK + k][g] = md == 2 ? 0.0f : sample_level<R, QBM>(u.st, P, lv, b, q0, g, k, md);
+        }
         __syncthreads();   // the stage is rebuilt by the next level / reused by the weight chunks
     }
     for (int i = C * QBM + tid; i < CPAD * QBM; i += NTM) T[i / QBM][i % QBM] = 0.0f;
