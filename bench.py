@@ -386,7 +386,7 @@ def main():
     dom = "build" if build_ms >= look_ms * iters else "lookup"
     roof = {k: kernels[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")}
     roof["kernel"] = dom
-    traffic, src = pmc_traffic("build_kernel" if dom == "build" else "lookup_staged")
+    traffic, src = pmc_traffic("build_kernel" if dom == "build" else "lookup_cols")
     roof["traffic"] = traffic
     if src:
         roof["traffic_source"] = src
