@@ -399,7 +399,7 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
     __syncthreads();
     for (int kc = 0; kc < nk; ++kc) {
         const int buf = kc & 1;
-        if (kc + 1 < nk) load_chunk((kc + 1) * KB);
+        if (kc + 1 < nk && P.dev_skip_epilogue < 3) load_chunk((kc + 1) * KB);
         const float* as = As + buf * KB * AS + wm * 64 + acol;
         const float* bs = Bs + buf * KB * BSS + wn * 64 + acol;
 #pragma unroll
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
             acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
             acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
         }
-        if (kc + 1 < nk) store_chunk(buf ^ 1);
+        if (kc + 1 < nk && P.dev_skip_epilogue < 4) store_chunk(buf ^ 1);
         __syncthreads();
     }
 
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                     }
         }
         __syncthreads();
-        if (P.dev_skip_epilogue == 1) continue;
+        if (P.dev_skip_epilogue == 1 || P.dev_skip_epilogue >= 3) continue;
         if (tc.band) epilogue_band<MR, NTS>(P, tc, Cs, tid, half * MR);
         else epilogue<MR, NTS>(P, tc, Cs, tid, half * MR);
         if (HALF && half == 0) __syncthreads();   // half 0 fully consumed before half 1 overwrites Cs
@@ -492,7 +492,9 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
     // dev knob for A/B ablation (tools/ab_build.py): ECORR_BUILD_SKIP_EPILOGUE=1 drops the pyramid
     // stores (output invalid); unset in production.
     const char* kskip = getenv("ECORR_BUILD_SKIP_EPILOGUE");
-    P.dev_skip_epilogue = kskip ? atoi(kskip) : 0;   // 2: level-0 stores only
+    // 2: level-0 stores only; 3: + no K-chunk global loads (LDS refilled from stale registers);
+    // 4: + no LDS refill (MFMA + fragment reads only)
+    P.dev_skip_epilogue = kskip ? atoi(kskip) : 0;
     const bool vec = (P.W % 4 == 0) && (P.q_count % 4 == 0) && ((uintptr_t)P.f1 % 16 == 0) &&
                      ((uintptr_t)P.f2 % 16 == 0);
     if ((uintptr_t)pyramid % 16 != 0) return ECORR_EINVAL;   // tile stores are 16-byte vectors

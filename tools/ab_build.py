@@ -15,6 +15,8 @@ VARIANTS = {
     "default": {},
     "nol0st": {"ECORR_BUILD_SKIP_EPILOGUE": "2"},
     "noepi": {"ECORR_BUILD_SKIP_EPILOGUE": "1"},
+    "noepi_noload": {"ECORR_BUILD_SKIP_EPILOGUE": "3"},
+    "noepi_noload_nostage": {"ECORR_BUILD_SKIP_EPILOGUE": "4"},
 }
 KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32", "ECORR_BUILD_NOBAND")
 B = int(os.environ.get("AB_BATCH", "16"))
@@ -27,7 +29,7 @@ times = {k: [] for k in VARIANTS}
 ref = None
 with torch.no_grad():
     names = list(VARIANTS)
-    for rnd in range(8):
+    for rnd in range(int(os.environ.get("AB_ROUNDS", "8"))):
         # rotate the order every round: the first variant of a round runs measurably slower
         for name in names[rnd % len(names):] + names[:rnd % len(names)]:
             env = VARIANTS[name]
@@ -36,7 +38,7 @@ with torch.no_grad():
             os.environ.update(env)
             blk = eraft_amd.CorrBlock(f1, f2)   # warm
             torch.cuda.synchronize()
-            if rnd == 0 and "noepi" not in name and "nol0" not in name:   # every variant must produce a valid pyramid (pooling exact vs level 0)
+            if rnd == 0 and "noepi" not in name and "nol0" not in name and "nnn" not in name:   # every variant must produce a valid pyramid (pooling exact vs level 0)
                 blk._levels_cache = None
                 lv0, lv1 = blk.corr_pyramid[0][:64, 0], blk.corr_pyramid[1][:64, 0]
                 p = (((lv0[:, 0::2, 0::2] + lv0[:, 0::2, 1::2]) + lv0[:, 1::2, 0::2]) + lv0[:, 1::2, 1::2]) * 0.25
