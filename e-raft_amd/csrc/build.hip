@@ -38,8 +38,8 @@ constexpr int P1S = 36, P2S = 12;  // LDS per-query strides of the pooled stagin
 
 // LDS floats for K chunk KB (double-buffered A and B, row strides AS / BS) and a C tile of MR
 // query rows.
-constexpr int smem_floats(int KB, int MR, int AS, int BS) {
-    return 2 * (KB * AS + KB * BS) > MR * CS ? 2 * (KB * AS + KB * BS) : MR * CS;
+constexpr int smem_floats(int KB, int MR, int AS, int BS, int NBUF = 2) {
+    return NBUF * (KB * AS + KB * BS) > MR * CS ? NBUF * (KB * AS + KB * BS) : MR * CS;
 }
 
 // 16-byte pyramid store; NTS = non-temporal: the 2 GB pyramid is not re-read by this kernel, and
@@ -318,14 +318,24 @@ __device__ __forceinline__ void epilogue_band(const BuildParams& P, const TileCo
 // KB = K chunk depth; HALF = C tile handled in two 64-query halves.  KB = 16 + HALF needs 34 KB of
 // LDS and <= 168 VGPRs, so 3 blocks (3 waves per SIMD) share a CU; KB = 32 uses 67.5 KB (2 blocks).
 // (A/B: v_mfma_f32_16x16x4_f32 tiles, bitwise the same result, ran 1% slower than 32x32x2.)
-template <bool VEC, int KB, bool HALF, bool NTS>
+//
+// GLDS: the K chunks go global -> LDS directly (buffer_load_dwordx4 ... lds, whose range check
+// zero-fills the padding) through 3 LDS buffers with two chunks in flight: each wave waits for its
+// own copies of chunk kc with a counted vmcnt, one raw barrier publishes them, and chunk kc + 2
+// is issued into the buffer chunk kc - 1 was read from.  No staging registers, no ds_write pass,
+// one barrier per chunk.  Needs VEC and byte offsets below 2^31 (launch_build checks).
+template <bool VEC, int KB, bool HALF, bool NTS, bool GLDS = false>
 __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) {
     constexpr int MR = HALF ? BM / 2 : BM;
     constexpr int AS = BM, BSS = BN;   // LDS row strides
     constexpr int NLD = (KB * BM / 4) / NT;   // float4 of A (and of B) per thread per chunk
-    __shared__ __attribute__((aligned(16))) float smem[smem_floats(KB, MR, AS, BSS)];
-    float* As = smem;                       // [2][KB][AS]
-    float* Bs = smem + 2 * KB * AS;         // [2][KB][BSS]
+    constexpr int NBUF = GLDS ? 3 : 2;
+    static_assert(!GLDS || (VEC && NLD == 2), "GLDS: vector path, 2 copies per operand per wave");
+    // ALL LDS in this one array: a second __shared__ object can make hipcc wait vmcnt(0) before
+    // every ds_read while a buffer_load ... lds is in flight (cdna_hip_programming.md trap 4(a))
+    __shared__ __attribute__((aligned(16))) float smem[smem_floats(KB, MR, AS, BSS, NBUF)];
+    float* As = smem;                       // [NBUF][KB][AS]
+    float* Bs = smem + NBUF * KB * AS;      // [NBUF][KB][BSS]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TileCoord tc = decode_tile(P, xcd_remap(blockIdx.x, gridDim.x));
@@ -394,12 +404,7 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
     const int arow = lane >> 5, acol = lane & 31;
     const int nk = (D + KB - 1) / KB;
 
-    load_chunk(0);
-    store_chunk(0);
-    __syncthreads();
-    for (int kc = 0; kc < nk; ++kc) {
-        const int buf = kc & 1;
-        if (kc + 1 < nk && P.dev_skip_epilogue < 3) load_chunk((kc + 1) * KB);
+    auto mfma_chunk = [&](int buf) {
         const float* as = As + buf * KB * AS + wm * 64 + acol;
         const float* bs = Bs + buf * KB * BSS + wn * 64 + acol;
 #pragma unroll
@@ -412,8 +417,60 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
             acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
             acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
         }
-        if (kc + 1 < nk && P.dev_skip_epilogue < 4) store_chunk(buf ^ 1);
+    };
+
+    if constexpr (GLDS) {
+        // copy i of this wave covers chunk rows kk = 2 wave + 8 i + (lane >> 5), 4 floats at
+        // column 4 (lane & 31): lane-linear 1 KB per wave-instruction, as LDS-DMA requires
+        const __amdgpu_buffer_rsrc_t rsa =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), 0, (int)((int64_t)D * QA * 4), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rsb =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Bm), 0, (int)((int64_t)D * Q * 4), 0x00020000);
+        constexpr int OOB = 0x7ffffff0;   // beyond any operand: reads (and lands in LDS) as 0
+        const int c = lane & 31, kl = lane >> 5;
+        const int m = tc.m0 + 4 * c;
+        const int y = tc.ty0 + (tc.band ? c >> 3 : c >> 2), x = tc.tx0 + 4 * (tc.band ? c & 7 : c & 3);
+        const bool aok = m < q_end, bok = y < H && x < W;
+        const int abase = m * 4, bbase = (y * W + x) * 4;
+        auto issue = [&](int kc) {
+            const int buf = kc % NBUF;
+#pragma unroll
+            for (int i = 0; i < NLD; ++i) {
+                const int kk = 2 * wave + 8 * i;   // wave-uniform first row of this copy
+                const int k = kc * KB + kk + kl;
+                const bool kin = k < D;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rsa, (__attribute__((address_space(3))) void*)(As + (buf * KB + kk) * AS), 16,
+                    aok && kin ? abase + k * (int)QA * 4 : OOB, 0, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rsb, (__attribute__((address_space(3))) void*)(Bs + (buf * KB + kk) * BSS), 16,
+                    bok && kin ? bbase + k * (int)Q * 4 : OOB, 0, 0, 0);
+            }
+        };
+        issue(0);
+        if (nk > 1) issue(1);
+        for (int kc = 0; kc < nk; ++kc) {
+            // this wave's copies of chunk kc have landed (those of kc + 1 may still fly) ...
+            if (kc + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // ... and every wave's have once all passed this barrier, which also retires the
+            // reads of chunk kc - 1, whose buffer chunk kc + 2 now overwrites
+            __builtin_amdgcn_s_barrier();
+            if (kc + 2 < nk && P.dev_skip_epilogue < 3) issue(kc + 2);
+            mfma_chunk(kc % NBUF);
+        }
+        __syncthreads();   // the C tile aliases the chunk buffers
+    } else {
+        load_chunk(0);
+        store_chunk(0);
         __syncthreads();
+        for (int kc = 0; kc < nk; ++kc) {
+            const int buf = kc & 1;
+            if (kc + 1 < nk && P.dev_skip_epilogue < 3) load_chunk((kc + 1) * KB);
+            mfma_chunk(buf);
+            if (kc + 1 < nk && P.dev_skip_epilogue < 4) store_chunk(buf ^ 1);
+            __syncthreads();
+        }
     }
 
     // ---- scaled accumulators -> LDS C tile [m][n]; C/D map: col = lane&31,
@@ -502,9 +559,16 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
     // 2-blocks-per-CU variant
     const char* kv = getenv("ECORR_BUILD_KB32");
     const bool kb32 = kv && atoi(kv) == 1;
+    // LDS-DMA staging (3% faster than register staging, tools/ab_build.py) whenever both operands'
+    // byte offsets fit the 31-bit buffer range; dev knob ECORR_BUILD_GLDS=0 selects the register-
+    // staged loop for A/B
+    const char* kg = getenv("ECORR_BUILD_GLDS");
+    const bool glds = !(kg && atoi(kg) == 0) && (int64_t)P.D * P.H * P.W * 4 < 0x7fff0000LL &&
+                      (int64_t)P.D * P.q_count * 4 < 0x7fff0000LL;
     const dim3 grid((unsigned)ntiles), block(NT);
     if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true>), grid, block, 0, stream, P);
     else if (kb32) hipLaunchKernelGGL((build_kernel<true, 32, false, true>), grid, block, 0, stream, P);
+    else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, true>), grid, block, 0, stream, P);
     else hipLaunchKernelGGL((build_kernel<true, 16, true, true>), grid, block, 0, stream, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ECORR_EHIP - (int)e;

@@ -13,12 +13,9 @@ import eraft_amd  # noqa: E402
 
 VARIANTS = {
     "default": {},
-    "nol0st": {"ECORR_BUILD_SKIP_EPILOGUE": "2"},
-    "noepi": {"ECORR_BUILD_SKIP_EPILOGUE": "1"},
-    "noepi_noload": {"ECORR_BUILD_SKIP_EPILOGUE": "3"},
-    "noepi_noload_nostage": {"ECORR_BUILD_SKIP_EPILOGUE": "4"},
+    "regstage": {"ECORR_BUILD_GLDS": "0"},
 }
-KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32", "ECORR_BUILD_NOBAND")
+KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32", "ECORR_BUILD_NOBAND", "ECORR_BUILD_GLDS")
 B = int(os.environ.get("AB_BATCH", "16"))
 H, W, D = 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)
