@@ -324,13 +324,22 @@ __device__ __forceinline__ void epilogue_band(const BuildParams& P, const TileCo
 // own copies of chunk kc with a counted vmcnt, one raw barrier publishes them, and chunk kc + 2
 // is issued into the buffer chunk kc - 1 was read from.  No staging registers, no ds_write pass,
 // one barrier per chunk.  Needs VEC and byte offsets below 2^31 (launch_build checks).
-template <bool VEC, int KB, bool HALF, bool NTS, bool GLDS = false>
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt fields at their "don't wait" maxima), N < 16
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 16, "vmcnt field");
+    __builtin_amdgcn_s_waitcnt(N | (7 << 4) | (15 << 8));
+}
+
+template <bool VEC, int KB, bool HALF, bool NTS, int GBUF = 0>
 __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) {
     constexpr int MR = HALF ? BM / 2 : BM;
     constexpr int AS = BM, BSS = BN;   // LDS row strides
     constexpr int NLD = (KB * BM / 4) / NT;   // float4 of A (and of B) per thread per chunk
-    constexpr int NBUF = GLDS ? 3 : 2;
-    static_assert(!GLDS || (VEC && NLD == 2), "GLDS: vector path, 2 copies per operand per wave");
+    constexpr bool GLDS = GBUF > 0;
+    constexpr int NBUF = GLDS ? GBUF : 2;   // GLDS: chunks kc .. kc + NBUF - 2 in flight
+    static_assert(!GLDS || (VEC && NLD >= 1 && NBUF >= 3 && 2 * NLD * (NBUF - 2) < 16),
+                  "GLDS: vector path, whole copies per wave, counted vmcnt in range");
     // ALL LDS in this one array: a second __shared__ object can make hipcc wait vmcnt(0) before
     // every ds_read while a buffer_load ... lds is in flight (cdna_hip_programming.md trap 4(a))
     __shared__ __attribute__((aligned(16))) float smem[smem_floats(KB, MR, AS, BSS, NBUF)];
@@ -447,16 +456,23 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                     bok && kin ? bbase + k * (int)Q * 4 : OOB, 0, 0, 0);
             }
         };
-        issue(0);
-        if (nk > 1) issue(1);
+        for (int kc = 0; kc < NBUF - 1 && kc < nk; ++kc) issue(kc);
         for (int kc = 0; kc < nk; ++kc) {
-            // this wave's copies of chunk kc have landed (those of kc + 1 may still fly) ...
-            if (kc + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // this wave's copies of chunk kc have landed (those of the later issued chunks may
+            // still fly: 2 NLD copies each) ...
+            const int after = min(nk, kc + NBUF - 1) - (kc + 1);
+            static_assert(NBUF <= 6, "wait ladder");
+            switch (after) {
+                case 0: wait_vmcnt<0>(); break;
+                case 1: wait_vmcnt<2 * NLD * (NBUF > 2 ? 1 : 0)>(); break;
+                case 2: wait_vmcnt<2 * NLD * (NBUF > 3 ? 2 : 0)>(); break;
+                case 3: wait_vmcnt<2 * NLD * (NBUF > 4 ? 3 : 0)>(); break;
+                default: wait_vmcnt<2 * NLD * (NBUF > 5 ? 4 : 0)>(); break;
+            }
             // ... and every wave's have once all passed this barrier, which also retires the
-            // reads of chunk kc - 1, whose buffer chunk kc + 2 now overwrites
+            // reads of chunk kc - 1, whose buffer chunk kc + NBUF - 1 now overwrites
             __builtin_amdgcn_s_barrier();
-            if (kc + 2 < nk && P.dev_skip_epilogue < 3) issue(kc + 2);
+            if (kc + NBUF - 1 < nk && P.dev_skip_epilogue < 3) issue(kc + NBUF - 1);
             mfma_chunk(kc % NBUF);
         }
         __syncthreads();   // the C tile aliases the chunk buffers
@@ -568,7 +584,7 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
     const dim3 grid((unsigned)ntiles), block(NT);
     if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true>), grid, block, 0, stream, P);
     else if (kb32) hipLaunchKernelGGL((build_kernel<true, 32, false, true>), grid, block, 0, stream, P);
-    else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, true>), grid, block, 0, stream, P);
+    else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3>), grid, block, 0, stream, P);
     else hipLaunchKernelGGL((build_kernel<true, 16, true, true>), grid, block, 0, stream, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ECORR_EHIP - (int)e;

@@ -51,9 +51,14 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
     __shared__ struct {
         WS st;
     } u;
-    __shared__ __attribute__((aligned(16))) float T[CPAD][QBM];
+    // row stride QBM + 4: the GEMM's B reads (lanes 0-31 row r, lanes 32-63 row r + 8) land in
+    // opposite bank halves; the lookup phase writes rows r and r + 8 from one wave for the same
+    // reason (a wave's two 32-query halves take rows 8 apart, see below)
+    constexpr int TS = QBM + 4;
+    __shared__ __attribute__((aligned(16))) float T[CPAD][TS];
 
     const int tid = threadIdx.x, g = tid % QBM, part = tid / QBM, lane = tid & 63, wave = tid >> 6;
+    const int half = part & 1;
     const int b = blockIdx.y;
     const int q0 = blockIdx.x * QBM;
     const int C = P.C;
@@ -66,14 +71,22 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
             constexpr int K = WS::K, S = WS::S;
             const int o0 = u.st.org[g][0], o1 = u.st.org[g][1];
             const float* wq = u.st.win + g * WS::SP;
-            for (int k = part; k < KK; k += NTM / QBM) {
+            // rows of each 16-row block: wave w, half h takes w + 8h and w + 4 + 8h
+            for (int k0 = 0; k0 < KK; k0 += 2 * NTM / QBM)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int k = k0 + wave + 4 * e + 8 * half;
+                if (k >= KK) continue;
                 const int a = k / K, bb = k - a * K;
                 const float* c = wq + ((int)u.st.fy[g][bb] - o1) * S + ((int)u.st.fx[g][a] - o0);
                 T[lv * KK + k][g] = blend(c[0], c[1], c[S], c[S + 1], u.st.wx[g][a], u.st.wy[g][bb]);
             }
         } else {
-            for (int k = part; k < KK; k += NTM / QBM)
-                T[lv * KK + k][g] = md == 2 ? 0.0f : sample_level<R, QBM>(u.st, P, lv, b, q0, g, k, md);
+            for (int k0 = 0; k0 < KK; k0 += 2 * NTM / QBM)
+                for (int e = 0; e < 2; ++e) {
+                    const int k = k0 + wave + 4 * e + 8 * half;
+                    if (k < KK) T[lv * KK + k][g] = md == 2 ? 0.0f : sample_level<R, QBM>(u.st, P, lv, b, q0, g, k, md);
+                }
         }
         __syncthreads();   // the stage is rebuilt by the next level / reused by the weight chunks
     }
