@@ -111,6 +111,85 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols(LookupParams P) {
     }
 }
 
+// lookup_cols with the coordinate chains in registers instead of LDS: every thread computes the
+// 2r+1 y chains and the x chains of its own columns (+ the two x end points for the window
+// check) itself, so the only LDS is the windows and their origins (31.7 KB at r = 4: 5 blocks per
+// CU instead of 4).  Same arithmetic, same bits.
+template <int R, int QB>
+__global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
+    constexpr int NTQ = 3 * QB, K = 2 * R + 1, AP = K / 3;
+    static_assert(K % 3 == 0 && QB == kWave, "one wave per part, whole columns per part");
+    using WB = WindowBuf<R, QB>;
+    constexpr int S = WB::S, SP = WB::SP, KK = WB::KK;
+    __shared__ WB st;
+    const int tid = threadIdx.x, g = tid % QB;
+    const int part = __builtin_amdgcn_readfirstlane(tid / QB);   // wave-uniform
+    const int lv = blockIdx.y, b = blockIdx.z;
+    const int q0 = blockIdx.x * QB;
+    const int p = q0 + g;
+    const bool valid = p < P.q_count;
+
+    // ---- phase 0 (registers): this thread's chains
+    float fy[K], wy[K], fx[AP], wx[AP], x0 = 0.0f, xl = 0.0f;
+    if (valid) {
+        const int64_t Q = P.q_count;
+        const float inv = 1.0f / (float)(1 << lv);  // coords / 2**i is an exact scaling
+        const float cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
+        const float cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);
+        const float wm1 = (float)(P.lw[lv] - 1), hm1 = (float)(P.lh[lv] - 1);
+#pragma unroll
+        for (int bb = 0; bb < K; ++bb) coord_chain<R>(cy, bb, hm1, fy[bb], wy[bb]);
+#pragma unroll
+        for (int ai = 0; ai < AP; ++ai) coord_chain<R>(cx, part * AP + ai, wm1, fx[ai], wx[ai]);
+        float dummy;
+        coord_chain<R>(cx, 0, wm1, x0, dummy);
+        coord_chain<R>(cx, K - 1, wm1, xl, dummy);
+    }
+    int org[3];
+    window_origin<S>(valid, x0, xl, fy[0], fy[K - 1], org);
+    if (part == 0) {
+        st.org[g][0] = org[0];
+        st.org[g][1] = org[1];
+        st.org[g][2] = org[2];
+    }
+    __syncthreads();
+    stage_windows<R, QB, NTQ>(st, P, lv, b, q0, tid);
+
+    const int md = org[2] & 0xff;
+    if (md == 2) return;   // past the range (no barrier follows)
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        P.out + (int64_t)b * P.C * P.q_count, 0, P.C * P.q_count * 4, 0x00020000);
+    const int voff = p * 4;
+    const int sbase = lv * KK * P.q_count * 4;
+    if (md == 0) {
+        int yo[K];
+#pragma unroll
+        for (int bb = 0; bb < K; ++bb) yo[bb] = ((int)fy[bb] - org[1]) * S;
+        const float* wq = st.win + g * SP;
+#pragma unroll
+        for (int ai = 0; ai < AP; ++ai) {
+            const int a = part * AP + ai;
+            const float* wc = wq + ((int)fx[ai] - org[0]);
+#pragma unroll
+            for (int bb = 0; bb < K; ++bb) {
+                const float* c = wc + yo[bb];
+                const float v = blend(c[0], c[1], c[S], c[S + 1], wx[ai], wy[bb]);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
+                                                      sbase + (a * K + bb) * P.q_count * 4, 2);
+            }
+        }
+    } else {   // coordinates that do not fit the window: exact direct gather
+#pragma unroll
+        for (int ai = 0; ai < AP; ++ai)
+#pragma unroll
+            for (int bb = 0; bb < K; ++bb) {
+                const float v = sample_direct(P, lv, b, p, fx[ai], fy[bb], wx[ai], wy[bb]);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
+                                                      sbase + ((part * AP + ai) * K + bb) * P.q_count * 4, 2);
+            }
+    }
+}
+
 // Any radius: one thread per output element, direct gather (reference-shaped; used for radii
 // without a staged instantiation).
 __global__ __launch_bounds__(NT) void lookup_direct(LookupParams P, int B) {
@@ -204,8 +283,12 @@ int launch_lookup(const LookupParams& Pin, int B, hipStream_t stream) {
                       (int64_t)P.C * P.q_count * 4 < 0x7fffffff;
     if (cols) {
         const dim3 grid((unsigned)((P.q_count + 63) / 64), (unsigned)P.levels, (unsigned)B);
-        if (P.radius == 4) hipLaunchKernelGGL((lookup_cols<4, 64>), grid, dim3(192), 0, stream, P);
-        else hipLaunchKernelGGL((lookup_cols<1, 64>), grid, dim3(192), 0, stream, P);
+        // ECORR_LOOKUP_V=3 (dev, A/B): the LDS-chain kernel lookup_cols (2.8% slower)
+        if (kv && atoi(kv) == 3) {
+            if (P.radius == 4) hipLaunchKernelGGL((lookup_cols<4, 64>), grid, dim3(192), 0, stream, P);
+            else hipLaunchKernelGGL((lookup_cols<1, 64>), grid, dim3(192), 0, stream, P);
+        } else if (P.radius == 4) hipLaunchKernelGGL((lookup_cols_reg<4, 64>), grid, dim3(192), 0, stream, P);
+        else hipLaunchKernelGGL((lookup_cols_reg<1, 64>), grid, dim3(192), 0, stream, P);
     } else if (qb == 16) launch_staged<16>(P, B, stream);
     else launch_staged<64>(P, B, stream);
     return hip_status();

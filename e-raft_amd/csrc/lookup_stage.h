@@ -19,34 +19,76 @@
 
 namespace ecorr {
 
+// The staged windows of QB queries and their origins (all phase 1 needs).
 template <int R, int QB>
-struct WindowStage {
+struct WindowBuf {
     static constexpr int K = 2 * R + 1;   // samples per axis
     static constexpr int KK = K * K;
     static constexpr int S = 2 * R + 3;   // staged window side
     static constexpr int SS = S * S;
     static constexpr int SP = SS | 1;     // odd per-query stride: conflict-free lanes = queries
     float win[QB * SP];
-    float fx[QB][K], wx[QB][K], fy[QB][K], wy[QB][K];
     // per query: window origin x, y and (mode | needed cols << 8 | needed rows << 16), where mode
     // 0 = staged, 1 = direct gather (coordinates that do not fit the window), 2 = past the range.
     int org[QB][3];
 };
+
+// ... plus the per-query coordinate chains in LDS (kernels whose threads share them).
+template <int R, int QB>
+struct WindowStage : WindowBuf<R, QB> {
+    static constexpr int K = 2 * R + 1;
+    float fx[QB][K], wx[QB][K], fy[QB][K], wy[QB][K];
+};
+
+// One coordinate chain (corr.py:41-43, utils.py:11-12, grid_sampler unnormalize): sample o of the
+// axis whose scaled coordinate is cs = coords / 2^lv, on a level side of m1 + 1 pixels.
+template <int R>
+__device__ __forceinline__ void coord_chain(float cs, int o, float m1, float& f, float& wgt) {
+    const float c = __fadd_rn(cs, (float)(o - R));
+    const float v = unnormalize(c, m1, m1 * 0.5f);
+    f = floorf(v);
+    wgt = __fsub_rn(v, f);
+}
+
+// Phase 0b for one query from its first / last x and y floors: origin and mode word (WindowBuf::org).
+template <int S>
+__device__ __forceinline__ void window_origin(bool valid, float x0, float xl, float y0, float yl, int org[3]) {
+    int md = 2, X0 = 0, Y0 = 0, NX = 0, NY = 0;
+    if (valid) {
+        bool ok = fabsf(x0) < 1.0e7f && fabsf(y0) < 1.0e7f;  // false for NaN / inf / huge
+        // every step of the chain (exact-or-rounded add of the offset, the normalize /
+        // unnormalize roundings by positive factors, floor) is monotone, so the floors are
+        // non-decreasing in the offset and the end points bound the whole window
+        const float dx = xl - x0, dy = yl - y0;   // exact: integers < 2^24
+        ok &= (dx >= 0.0f) & (dx <= (float)(S - 2)) & (dy >= 0.0f) & (dy <= (float)(S - 2));
+        md = ok ? 0 : 1;
+        X0 = ok ? (int)x0 : 0;
+        Y0 = ok ? (int)y0 : 0;
+        // corners span [x0, floor(ix_last) + 1]: monotone round trip, so the last sample bounds it
+        NX = ok ? (int)dx + 2 : 0;
+        NY = ok ? (int)dy + 2 : 0;
+    }
+    org[0] = X0;
+    org[1] = Y0;
+    org[2] = md | (NX << 8) | (NY << 16);
+}
+
+template <int R, int QB, int NTQ>
+__device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const LookupParams& P, int lv, int b, int q0,
+                                              int tid);
 
 // Phases 0 and 1 for level lv of queries [q0, q0 + QB) of batch item b; ends with a barrier.
 template <int R, int QB, int NTQ>
 __device__ __forceinline__ void stage_level(WindowStage<R, QB>& st, const LookupParams& P, int lv, int b, int q0,
                                             int tid) {
     using WS = WindowStage<R, QB>;
-    constexpr int K = WS::K, S = WS::S, SP = WS::SP;
+    constexpr int K = WS::K, S = WS::S;
     constexpr int TPQ = NTQ / QB;   // threads per query
     const int g = tid % QB, part = tid / QB;
-    const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
+    const int h = P.lh[lv], w = P.lw[lv];
     const int p = q0 + g;
     const bool valid = p < P.q_count;
     const int64_t Q = P.q_count;   // coords slab stride
-    const int64_t hw = P.lsz[lv];  // floats per query image
-    const float* __restrict__ lvbase = P.lvl[lv] + ((int64_t)b * P.q_count + q0) * hw;
 
     // ---- phase 0: coordinate chains (corr.py:41-43, utils.py:11-12, grid_sampler unnormalize)
     if (valid) {
@@ -58,39 +100,29 @@ __device__ __forceinline__ void stage_level(WindowStage<R, QB>& st, const Lookup
         for (int j = part; j < 2 * K; j += TPQ) {
             const bool isx = j < K;
             const int o = isx ? j : j - K;
-            const float c = __fadd_rn(isx ? cx : cy, (float)(o - R));
-            const float m1 = isx ? wm1 : hm1;
-            const float v = unnormalize(c, m1, m1 * 0.5f);
-            const float f = floorf(v);
-            if (isx) { st.fx[g][o] = f; st.wx[g][o] = __fsub_rn(v, f); }
-            else     { st.fy[g][o] = f; st.wy[g][o] = __fsub_rn(v, f); }
+            float f, wgt;
+            coord_chain<R>(isx ? cx : cy, o, isx ? wm1 : hm1, f, wgt);
+            if (isx) { st.fx[g][o] = f; st.wx[g][o] = wgt; }
+            else     { st.fy[g][o] = f; st.wy[g][o] = wgt; }
         }
     }
     __syncthreads();
 
     // ---- phase 0b: window origin and fast/slow decision per query
-    if (part == 0) {
-        int md = 2, X0 = 0, Y0 = 0, NX = 0, NY = 0;
-        if (valid) {
-            const float x0 = st.fx[g][0], y0 = st.fy[g][0];
-            bool ok = fabsf(x0) < 1.0e7f && fabsf(y0) < 1.0e7f;  // false for NaN / inf / huge
-            // every step of the chain (exact-or-rounded add of the offset, the normalize /
-            // unnormalize roundings by positive factors, floor) is monotone, so the floors are
-            // non-decreasing in the offset and the end points bound the whole window
-            const float dx = st.fx[g][K - 1] - x0, dy = st.fy[g][K - 1] - y0;   // exact: integers < 2^24
-            ok &= (dx >= 0.0f) & (dx <= (float)(S - 2)) & (dy >= 0.0f) & (dy <= (float)(S - 2));
-            md = ok ? 0 : 1;
-            X0 = ok ? (int)x0 : 0;
-            Y0 = ok ? (int)y0 : 0;
-            // corners span [x0, floor(ix_last) + 1]: monotone round trip, so the last sample bounds it
-            NX = ok ? (int)(st.fx[g][K - 1] - x0) + 2 : 0;
-            NY = ok ? (int)(st.fy[g][K - 1] - y0) + 2 : 0;
-        }
-        st.org[g][0] = X0;
-        st.org[g][1] = Y0;
-        st.org[g][2] = md | (NX << 8) | (NY << 16);
-    }
+    if (part == 0) window_origin<S>(valid, st.fx[g][0], st.fx[g][K - 1], st.fy[g][0], st.fy[g][K - 1], st.org[g]);
     __syncthreads();
+    stage_windows<R, QB, NTQ>(st, P, lv, b, q0, tid);
+}
+
+// Phase 1 for level lv of queries [q0, q0 + QB) of batch item b, from st.org; ends with a barrier.
+template <int R, int QB, int NTQ>
+__device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const LookupParams& P, int lv, int b, int q0,
+                                              int tid) {
+    using WS = WindowBuf<R, QB>;
+    constexpr int S = WS::S, SP = WS::SP;
+    const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
+    const int64_t hw = P.lsz[lv];  // floats per query image
+    const float* __restrict__ lvbase = P.lvl[lv] + ((int64_t)b * P.q_count + q0) * hw;
 
     // ---- phase 1: stage windows, zeros outside the image (grid_sample padding_mode='zeros').
     // Work item = (query, window column); each item walks the S rows.  Loads are raw buffer loads
@@ -142,6 +174,17 @@ __device__ __forceinline__ void stage_level(WindowStage<R, QB>& st, const Lookup
     __syncthreads();
 }
 
+// Exact direct gather of one sample of query p (slab index) from its floors and weights, for
+// coordinates that do not fit the window (NaN / inf / huge: corner() range-checks in float).
+__device__ __forceinline__ float sample_direct(const LookupParams& P, int lv, int b, int p, float xa, float yb,
+                                               float wa, float nb) {
+    const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
+    const float* img = P.lvl[lv] + ((int64_t)b * P.q_count + p) * (int64_t)P.lsz[lv];
+    const float xa1 = __fadd_rn(xa, 1.0f), yb1 = __fadd_rn(yb, 1.0f);
+    return blend(corner(img, h, w, xa, yb, ntx), corner(img, h, w, xa1, yb, ntx),
+                 corner(img, h, w, xa, yb1, ntx), corner(img, h, w, xa1, yb1, ntx), wa, nb);
+}
+
 // Phase 2: sample k = a(2r+1) + b of query g (staged mode md = 0 or direct mode md = 1).
 template <int R, int QB>
 __device__ __forceinline__ float sample_level(const WindowStage<R, QB>& st, const LookupParams& P, int lv, int b,
@@ -155,11 +198,7 @@ __device__ __forceinline__ float sample_level(const WindowStage<R, QB>& st, cons
         const float* c = st.win + g * SP + ((int)yb - st.org[g][1]) * S + ((int)xa - st.org[g][0]);
         return blend(c[0], c[1], c[S], c[S + 1], wa, nb);
     }
-    const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
-    const float* img = P.lvl[lv] + ((int64_t)b * P.q_count + q0 + g) * (int64_t)P.lsz[lv];
-    const float xa1 = __fadd_rn(xa, 1.0f), yb1 = __fadd_rn(yb, 1.0f);
-    return blend(corner(img, h, w, xa, yb, ntx), corner(img, h, w, xa1, yb, ntx),
-                 corner(img, h, w, xa, yb1, ntx), corner(img, h, w, xa1, yb1, ntx), wa, nb);
+    return sample_direct(P, lv, b, q0 + g, xa, yb, wa, nb);
 }
 
 }  // namespace ecorr

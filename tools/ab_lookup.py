@@ -12,7 +12,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import eraft_amd  # noqa: E402
 
-VARIANTS = {"cols3": {}, "staged4": {"ECORR_LOOKUP_V": "4"}, "cols3_skipall": {"ECORR_LOOKUP_SKIP": "15"}}
+VARIANTS = {"cols3reg": {}, "cols3": {"ECORR_LOOKUP_V": "3"}, "staged4": {"ECORR_LOOKUP_V": "4"}}
 KNOBS = ("ECORR_LOOKUP_QB", "ECORR_LOOKUP_V", "ECORR_LOOKUP_SKIP")
 B, H, W, D = int(os.environ.get("AB_BATCH", "16")), 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)
@@ -28,7 +28,7 @@ with torch.no_grad():
     times = {k: [] for k in VARIANTS}
     ref = None
     names = list(VARIANTS)
-    for rnd in range(6):
+    for rnd in range(int(os.environ.get("AB_ROUNDS", "6"))):
         # rotate the order every round: the first variant of a round runs measurably slower
         for name in names[rnd % len(names):] + names[:rnd % len(names)]:
             env = VARIANTS[name]
