@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -36,6 +36,10 @@ SYMBOLS = {
                                   ctypes.POINTER(_i64)]),
     # (fmap1, fmap2, B, D, H, W, q_count, levels, pyramid, stream)
     "ecorr_build": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
+    # (B, H, W, q_count, bytes*)
+    "ecorr_build_split_workspace_size": (_i, [_i, _i, _i, _i, ctypes.POINTER(_i64)]),
+    # (fmap1, fmap2, B, D, H, W, q_count, levels, pyramid, workspace, stream)
+    "ecorr_build_split": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     # (pyramid, coords, B, H, W, q_count, levels, radius, out, stream)
     "ecorr_lookup": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
     # (pyramid, coords, B, H, W, q_count, levels, radius, weight[O][C], bias, O, out, stream)
@@ -110,3 +114,46 @@ def layout(rows: int, H: int, W: int, levels: int):
 
 def stream_of(t: torch.Tensor):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+# Which GEMM builds level 0 (include/ecorr.h): "split" = ecorr_build_split (f16 matrix cores on
+# per-pixel-scaled hi/lo halves of every fp32 operand; error vs fp64 below the fp32 path's),
+# "fp32" = ecorr_build (fp32 MFMA, an exact k-ordered fmaf chain per element).  Both meet the
+# north star's 1e-5 bar against the reference's fp32 GEMM; ECORR_BUILD_MODE overrides.
+BUILD_MODES = ("split", "fp32")
+_build_mode = os.environ.get("ECORR_BUILD_MODE", "split")
+if _build_mode not in BUILD_MODES:
+    raise ValueError(f"ECORR_BUILD_MODE={_build_mode!r} not in {BUILD_MODES}")
+
+
+def set_build_mode(mode: str):
+    global _build_mode
+    if mode not in BUILD_MODES:
+        raise ValueError(f"build mode {mode!r} not in {BUILD_MODES}")
+    _build_mode = mode
+
+
+def build_mode() -> str:
+    return _build_mode
+
+
+def build_pyramid(fmap1, fmap2, B, D, H, W, q_count, levels, off, what, mode=None):
+    """Allocate the pyramid (levels at off[i], plus the split build's exponent scratch as a tail
+    past off[-1]) on fmap2's device and build it on the current stream.  Returns the tensor."""
+    mode = mode or _build_mode
+    if mode not in BUILD_MODES:
+        raise ValueError(f"build mode {mode!r} not in {BUILD_MODES}")
+    tail = 0
+    if mode == "split":
+        nbytes = _i64()
+        check(lib().ecorr_build_split_workspace_size(B, H, W, q_count, ctypes.byref(nbytes)), what)
+        tail = (nbytes.value + 127) // 128 * 32   # floats, whole 128-byte lines
+    pyr = torch.empty(off[-1] + tail, dtype=torch.float32, device=fmap2.device)
+    st = stream_of(fmap2)
+    if mode == "split":
+        check(lib().ecorr_build_split(fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, q_count, levels,
+                                      pyr.data_ptr(), pyr.data_ptr() + 4 * off[-1], st), what)
+    else:
+        check(lib().ecorr_build(fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, q_count, levels,
+                                pyr.data_ptr(), st), what)
+    return pyr

@@ -61,10 +61,8 @@ class CorrBlock:
         Q = H * W
         self._h, self._w, self._off = _lib.layout(B * Q, H, W, num_levels)
         with torch.cuda.device(self._device):
-            self._pyramid = torch.empty(self._off[-1], dtype=torch.float32, device=self._device)
-            _lib.check(_lib.lib().ecorr_build(
-                fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, Q, num_levels,
-                self._pyramid.data_ptr(), _lib.stream_of(fmap1)), "CorrBlock build")
+            self._pyramid = _lib.build_pyramid(fmap1, fmap2, B, D, H, W, Q, num_levels, self._off,
+                                               "CorrBlock build")
         self._rows = B * Q
         self._levels_cache = None
 

@@ -97,8 +97,10 @@ ECORR_EXPORT int ecorr_pyramid_formats(int H, int W, int levels, int* ntx) {
     return ECORR_OK;
 }
 
-ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
-                             int levels, float* pyramid, void* stream) {
+namespace {
+
+int build_common(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count, int levels,
+                 float* pyramid, void* workspace, void* stream) {
     if (!fmap1 || !fmap2 || !pyramid || B <= 0 || D <= 0) return ECORR_EINVAL;
     if (!q_count_ok(H, W, q_count)) return ECORR_EINVAL;
     PyrGeom g;
@@ -119,7 +121,31 @@ ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int 
     const float mant = frexpf(s, &e);
     P.scale_is_mul = (mant == 0.5f) ? 1 : 0;
     P.scale = P.scale_is_mul ? 1.0f / s : s;
+    if (workspace) {
+        if (B > 65535 || ((uintptr_t)workspace & 3)) return ECORR_EINVAL;
+        P.ex1 = static_cast<int*>(workspace);
+        P.ex2 = P.ex1 + (int64_t)B * q_count;
+    }
     return launch_build(P, B, g, pyramid, (hipStream_t)stream);
+}
+
+}  // namespace
+
+ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
+                             int levels, float* pyramid, void* stream) {
+    return build_common(fmap1, fmap2, B, D, H, W, q_count, levels, pyramid, nullptr, stream);
+}
+
+ECORR_EXPORT int ecorr_build_split_workspace_size(int B, int H, int W, int q_count, int64_t* bytes) {
+    if (!bytes || B <= 0 || B > 65535 || !q_count_ok(H, W, q_count)) return ECORR_EINVAL;
+    *bytes = build_split_workspace_bytes(B, H, W, q_count);
+    return ECORR_OK;
+}
+
+ECORR_EXPORT int ecorr_build_split(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
+                                   int levels, float* pyramid, void* workspace, void* stream) {
+    if (!workspace) return ECORR_EINVAL;
+    return build_common(fmap1, fmap2, B, D, H, W, q_count, levels, pyramid, workspace, stream);
 }
 
 namespace {

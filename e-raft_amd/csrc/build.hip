@@ -53,6 +53,23 @@ __device__ __forceinline__ void st(V* p, V v) {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+
+// Split mode: x * 2^e = hi + lo + O(2^-22 |x|), hi = f16(x 2^e), lo = f16(x 2^e - hi) (the
+// subtraction is exact).  e puts the pixel's largest |value| in [2^14, 2^15), so hi never
+// overflows and lo stays normal for all but values 2^17 below that maximum.
+__device__ __forceinline__ void split_f16(const float (&v)[8], float s, halfx8& hi, halfx8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = v[j] * s;
+        const _Float16 h = (_Float16)x;
+        hi[j] = h;
+        lo[j] = (_Float16)(x - (float)h);
+    }
+}
+
+// 2^e as a float, e in [-126, 127]
+__device__ __forceinline__ float exp2i(int e) { return __int_as_float((e + 127) << 23); }
 
 __device__ __forceinline__ float pool4(float a, float b, float c, float d) {
     return __fmul_rn(__fadd_rn(__fadd_rn(__fadd_rn(a, b), c), d), 0.25f);
@@ -331,7 +348,13 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt(N | (7 << 4) | (15 << 8));
 }
 
-template <bool VEC, int KB, bool HALF, bool NTS, int GBUF = 0>
+// SPLIT: the fp32 operands are split into f16 hi + lo per fragment (split_f16, per-pixel
+// power-of-two scales from fmap_exp_kernel) and each 16-deep K chunk runs 3 v_mfma_f32_32x32x16_f16
+// per 32x32 tile (lo*hi, hi*lo, hi*hi; lo*lo is below fp32 rounding) instead of 8 fp32 MFMAs:
+// 3 x 32 vs 8 x 64 matrix-core cycles.  The fragment reads are the fp32 path's: lane (r, h) takes
+// k = 2j + h as element j, the same permutation on both operands.  Normwise error vs fp64 is
+// below the fp32 path's; the result is scaled back by 2^-(e1+e2) exactly.
+template <bool VEC, int KB, bool HALF, bool NTS, int GBUF = 0, bool SPLIT = false>
 __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) {
     constexpr int MR = HALF ? BM / 2 : BM;
     constexpr int AS = BM, BSS = BN;   // LDS row strides
@@ -342,9 +365,11 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                   "GLDS: vector path, whole copies per wave, counted vmcnt in range");
     // ALL LDS in this one array: a second __shared__ object can make hipcc wait vmcnt(0) before
     // every ds_read while a buffer_load ... lds is in flight (cdna_hip_programming.md trap 4(a))
-    __shared__ __attribute__((aligned(16))) float smem[smem_floats(KB, MR, AS, BSS, NBUF)];
+    constexpr int SM = smem_floats(KB, MR, AS, BSS, NBUF);
+    __shared__ __attribute__((aligned(16))) float smem[SM + (SPLIT ? BM + BN : 0)];
     float* As = smem;                       // [NBUF][KB][AS]
     float* Bs = smem + NBUF * KB * AS;      // [NBUF][KB][BSS]
+    int* exs = reinterpret_cast<int*>(smem + SM);   // SPLIT: exponents of the BM queries, BN targets
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TileCoord tc = decode_tile(P, xcd_remap(blockIdx.x, gridDim.x));
@@ -354,6 +379,20 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
     const int64_t QA = P.q_count;
     const float* __restrict__ A = P.f1 + (int64_t)tc.b * D * QA;
     const float* __restrict__ Bm = P.f2 + (int64_t)tc.b * D * Q;
+    if constexpr (SPLIT) {
+        // LDS column n of the B tile is target (y, x) as the loads below map it
+        const int t = threadIdx.x;
+        int e = 0;
+        if (t < BM) {
+            if (tc.m0 + t < P.q_count) e = P.ex1[(int64_t)tc.b * P.q_count + tc.m0 + t];
+        } else {
+            const int n = t - BM, c = n >> 2;
+            const int y = tc.ty0 + (tc.band ? c >> 3 : c >> 2), x = tc.tx0 + 4 * (tc.band ? c & 7 : c & 3) + (n & 3);
+            if (y < P.H && x < P.W) e = P.ex2[(int64_t)tc.b * Q + (int64_t)y * P.W + x];
+        }
+        exs[t] = e;
+        __syncthreads();
+    }
 
     // ---- global -> register staging: NLD float4 of A and of B per thread per K chunk ----
     floatx4 ra[NLD], rb[NLD];
@@ -413,9 +452,49 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
     const int arow = lane >> 5, acol = lane & 31;
     const int nk = (D + KB - 1) / KB;
 
+    float sa0 = 1.f, sa1 = 1.f, sb0 = 1.f, sb1 = 1.f;
+    if constexpr (SPLIT) {
+        sa0 = exp2i(exs[wm * 64 + acol]);
+        sa1 = exp2i(exs[wm * 64 + 32 + acol]);
+        sb0 = exp2i(exs[BM + wn * 64 + acol]);
+        sb1 = exp2i(exs[BM + wn * 64 + 32 + acol]);
+    }
+
     auto mfma_chunk = [&](int buf) {
         const float* as = As + buf * KB * AS + wm * 64 + acol;
         const float* bs = Bs + buf * KB * BSS + wn * 64 + acol;
+        if constexpr (SPLIT) {
+#pragma unroll
+            for (int k16 = 0; k16 < KB; k16 += 16) {
+                float va0[8], va1[8], vb0[8], vb1[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int ro = k16 + 2 * j + arow;
+                    va0[j] = as[ro * AS];
+                    va1[j] = as[ro * AS + 32];
+                    vb0[j] = bs[ro * BSS];
+                    vb1[j] = bs[ro * BSS + 32];
+                }
+                halfx8 a0h, a0l, a1h, a1l, b0h, b0l, b1h, b1l;
+                split_f16(va0, sa0, a0h, a0l);
+                split_f16(va1, sa1, a1h, a1l);
+                split_f16(vb0, sb0, b0h, b0l);
+                split_f16(vb1, sb1, b1h, b1l);
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0l, b0h, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0l, b1h, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l, b0h, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l, b1h, acc[1][1], 0, 0, 0);
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b0l, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b1l, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b0l, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b1l, acc[1][1], 0, 0, 0);
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b0h, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b1h, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b0h, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b1h, acc[1][1], 0, 0, 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int kk = 0; kk < KB; kk += 2) {
             const int ro = kk + arow;
@@ -504,7 +583,9 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                     for (int r = 0; r < 16; ++r) {
                         const int m = mb + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
                         const int n = wn * 64 + j * 32 + acol;
-                        const float v = acc[i][j][r];
+                        float v = acc[i][j][r];
+                        // SPLIT: undo the 2^(e1+e2) operand scaling (exact unless subnormal)
+                        if constexpr (SPLIT) v = ldexpf(v, -(exs[(HALF ? half * 64 : 0) + m] + exs[BM + n]));
                         Cs[m * CS + n] = P.scale_is_mul ? __fmul_rn(v, P.scale) : __fdiv_rn(v, P.scale);
                     }
         }
@@ -534,7 +615,37 @@ __global__ __launch_bounds__(256) void pool2_kernel(const float* __restrict__ in
     }
 }
 
+// Split-mode exponent pass: ex[b][n] = 15 - E with max_d |x[b][d][n]| = f 2^E, f in [0.5, 1)
+// (so the pixel's largest scaled value lies in [2^14, 2^15)); 0 for all-zero or non-finite maxima
+// (NaN inputs propagate through the GEMM as in the reference).  x: [B][D][N].  Block = 64 pixels
+// x 4 channel groups (coalesced 256-byte rows per wave), grid (ceil(N / 64), B).
+__global__ __launch_bounds__(256) void fmap_exp_kernel(const float* __restrict__ x, int D, int64_t N,
+                                                       int* __restrict__ ex) {
+    __shared__ float red[4][64];
+    const int b = blockIdx.y, l = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t n = (int64_t)blockIdx.x * 64 + l;
+    float m = 0.f;
+    if (n < N) {
+        const float* p = x + (int64_t)b * D * N + n;
+        for (int d = g; d < D; d += 4) m = fmaxf(m, fabsf(p[(int64_t)d * N]));
+    }
+    red[g][l] = m;
+    __syncthreads();
+    if (g == 0 && n < N) {
+        m = fmaxf(fmaxf(red[0][l], red[1][l]), fmaxf(red[2][l], red[3][l]));
+        int E = 0;
+        frexpf(m, &E);
+        int e = (m > 0.f && m <= 3.4028235e38f) ? 15 - E : 0;
+        e = e < -126 ? -126 : (e > 126 ? 126 : e);
+        ex[(int64_t)b * N + n] = e;
+    }
+}
+
 }  // namespace
+
+int64_t build_split_workspace_bytes(int B, int H, int W, int q_count) {
+    return ((int64_t)B * q_count + (int64_t)B * H * W) * (int64_t)sizeof(int);
+}
 
 int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid, hipStream_t stream) {
     BuildParams P = P0;
@@ -582,7 +693,16 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
     const bool glds = !(kg && atoi(kg) == 0) && (int64_t)P.D * P.H * P.W * 4 < 0x7fff0000LL &&
                       (int64_t)P.D * P.q_count * 4 < 0x7fff0000LL;
     const dim3 grid((unsigned)ntiles), block(NT);
-    if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true>), grid, block, 0, stream, P);
+    if (P.ex1) {
+        const int64_t Q = (int64_t)P.H * P.W;
+        hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((P.q_count + 63) / 64), B), dim3(256), 0, stream, P.f1,
+                           P.D, (int64_t)P.q_count, P.ex1);
+        hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((Q + 63) / 64), B), dim3(256), 0, stream, P.f2, P.D, Q,
+                           P.ex2);
+        if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true, 0, true>), grid, block, 0, stream, P);
+        else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true>), grid, block, 0, stream, P);
+        else hipLaunchKernelGGL((build_kernel<true, 16, true, true, 0, true>), grid, block, 0, stream, P);
+    } else if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true>), grid, block, 0, stream, P);
     else if (kb32) hipLaunchKernelGGL((build_kernel<true, 32, false, true>), grid, block, 0, stream, P);
     else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3>), grid, block, 0, stream, P);
     else hipLaunchKernelGGL((build_kernel<true, 16, true, true>), grid, block, 0, stream, P);

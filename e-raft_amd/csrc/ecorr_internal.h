@@ -27,6 +27,10 @@ struct BuildParams {
     int q_count;        // query pixels in the fmap1 slab
     float scale;        // sqrt(D) (divide) or 1/sqrt(D) when sqrt(D) is a power of two (multiply)
     int scale_is_mul;
+    // split mode (ecorr_build_split): per-pixel power-of-two exponents of fmap1 ([B][q_count]) and
+    // fmap2 ([B][H*W]) written by the exponent pass; null = the fp32-MFMA fmaf-chain build
+    int* ex1;
+    int* ex2;
     // filled by launch_build
     int n_mt, n_nt, n_ntx, n_tiles;
     int n_reg, band_y0;  // regular (8 x 16) n-tiles per m-tile; first row of the 4-row band tiles
@@ -39,6 +43,7 @@ struct BuildParams {
 };
 
 int launch_build(const BuildParams& P, int B, const PyrGeom& g, float* pyramid, hipStream_t stream);
+int64_t build_split_workspace_bytes(int B, int H, int W, int q_count);
 
 struct LookupParams {
     const float* coords;  // [B][2][q_count]

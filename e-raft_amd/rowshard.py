@@ -103,10 +103,8 @@ class RowShardedCorrBlock:
         self.q_count = self.counts[self.rank] * W
         self._h, self._w, self._off = _lib.layout(B * self.q_count, H, W, num_levels)
         with torch.cuda.device(self._device):
-            self._pyramid = torch.empty(self._off[-1], dtype=torch.float32, device=self._device)
-            _lib.check(_lib.lib().ecorr_build(
-                fmap1_rows.data_ptr(), fmap2.data_ptr(), B, D, H, W, self.q_count, num_levels,
-                self._pyramid.data_ptr(), _lib.stream_of(fmap2)), "RowShardedCorrBlock build")
+            self._pyramid = _lib.build_pyramid(fmap1_rows, fmap2, B, D, H, W, self.q_count, num_levels,
+                                               self._off, "RowShardedCorrBlock build")
         self._levels_cache = None
 
     @property

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 8
+#define ECORR_ABI_VERSION 9
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -63,6 +63,18 @@ int ecorr_pyramid_layout(int64_t rows, int H, int W, int levels, int* h, int* w,
  * Replaces: CorrBlock.__init__ (corr.py:13-27) and CorrBlock.corr (corr.py:52-60). */
 int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
                 int levels, float* pyramid, void* stream);
+
+/* Same result contract as ecorr_build (level 0 within the 1e-5 normwise bar of the reference's
+ * fp32 GEMM, levels 1.. pooled bit-exactly from it), computed on the f16 matrix cores: each fp32
+ * operand is scaled by a per-pixel power of two and split into f16 hi + lo, and every product is
+ * summed as lo*hi + hi*lo + hi*hi in fp32 -- error vs fp64 below the fp32-MFMA path's.  Per-pixel
+ * scales depend only on that pixel's D values, so row-sharded and whole builds agree bit for bit.
+ * workspace: ecorr_build_split_workspace_size() bytes of device memory (4-byte aligned, scratch
+ * for the exponents; free after the call completes on `stream`).  B <= 65535.
+ * Replaces: CorrBlock.__init__ (corr.py:13-27) and CorrBlock.corr (corr.py:52-60). */
+int ecorr_build_split_workspace_size(int B, int H, int W, int q_count, int64_t* bytes);
+int ecorr_build_split(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
+                      int levels, float* pyramid, void* workspace, void* stream);
 
 /* Radius-r lookup: out float[B][levels*(2r+1)^2][q_count] (= [B][C][H][W] when q_count = H*W),
  * channel 81*i + 9*a + b (r = 4) = bilinear sample of level i at (x/2^i + a - r, y/2^i + b - r),

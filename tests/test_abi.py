@@ -116,3 +116,18 @@ def test_tile_untile_roundtrip():
         # element (y, x) of image r lives at r*hp*wp + ((y//4)*(wp//8) + x//8)*32 + (y%4)*8 + x%8
         r, y, x = 2, h - 1, w - 1
         assert flat[r * hp * wp + ((y // 4) * (wp // 8) + x // 8) * 32 + (y % 4) * 8 + x % 8] == lv[r, y, x]
+
+
+def test_split_build_arguments(ea):
+    from eraft_amd import _lib
+    L = _lib.lib()
+    n = ctypes.c_int64()
+    assert L.ecorr_build_split_workspace_size(16, 60, 80, 4800, ctypes.byref(n)) == 0
+    assert n.value == 4 * (16 * 4800 + 16 * 4800)
+    assert L.ecorr_build_split_workspace_size(4, 92, 160, 1840, ctypes.byref(n)) == 0
+    assert n.value == 4 * (4 * 1840 + 4 * 92 * 160)
+    assert L.ecorr_build_split_workspace_size(0, 60, 80, 4800, ctypes.byref(n)) == _lib.ECORR_EINVAL
+    assert L.ecorr_build_split_workspace_size(1, 60, 80, 4801, ctypes.byref(n)) == _lib.ECORR_EINVAL
+    assert L.ecorr_build_split(8, 8, 1, 256, 8, 8, 64, 4, 8, None, None) == _lib.ECORR_EINVAL
+    with pytest.raises(ValueError):
+        _lib.set_build_mode("bf16")
