@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark of the E-RAFT CorrBlock hot path on MI355X (BASELINE.json metric).
 
-One step = one pass of the hot path over one batch: CorrBlock build (fp32-MFMA GEMM + fused
-pyramid) followed by the 12 GRU-iteration lookups, exactly the call pattern of ERAFT.forward
+One step = one pass of the hot path over one batch: CorrBlock build (split-f16 or fp32 MFMA GEMM
++ fused pyramid; ECORR_BUILD_MODE) followed by the 12 GRU-iteration lookups, exactly the call pattern of ERAFT.forward
 (eraft.py:107, 126-128), with inputs already resident in HBM.
 
   default (--mode batch): BASELINE configs[1] at N=1 -- DSEC 480x640 (fmaps 256 x 60 x 80), batch
@@ -35,6 +35,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "flow pairs/sec (DSEC 480×640, 12 iters) at 1/8 GPUs; CorrBlock % roofline"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix, spec (dense)
+PEAK_F16_MFMA_TFLOPS = 2516.6   # MI355X_MICROARCH.md: BF16/F16 matrix, dense (1024 flop/clk/SIMD)
+SPLIT_MFMA_PER_PRODUCT = 3      # split build: lo*hi + hi*lo + hi*hi on the f16 matrix cores
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak, spec
 
 
@@ -61,13 +63,26 @@ def parse():
 
 
 def algorithmic(B, D, H, W, L=4, r=4, q=None):
-    """build flops 2*B*q*Q*D; lookup bytes B*q*[L(2r+2)^2*4 + L(2r+1)^2*4 + 8]
-    (q = query pixels served, Q = H*W targets)."""
+    """build flops 2*B*q*Q*D; build bytes 4*B*D*(q + Q) (fmaps in) + 4*B*q*sum(h_i*w_i)
+    (pyramid out); lookup bytes B*q*[L(2r+2)^2*4 + L(2r+1)^2*4 + 8] (q = query pixels served,
+    Q = H*W targets)."""
     Q = H * W
     q = Q if q is None else q
     flops = 2.0 * B * q * Q * D
+    hs, ws, pix = H, W, 0
+    for i in range(L):
+        if i:
+            hs, ws = hs // 2, ws // 2
+        pix += hs * ws
+    build_bytes = 4.0 * B * D * (q + Q) + 4.0 * B * q * pix
     look_bytes = B * q * (L * (2 * r + 2) ** 2 * 4 + L * (2 * r + 1) ** 2 * 4 + 2 * 4)
-    return flops, look_bytes
+    return flops, build_bytes, look_bytes
+
+
+def build_floors(flops, build_bytes, mode):
+    """Ideal build time (s) on each roof: the matrix cores at the mode's rate, HBM for the bytes."""
+    mfma_peak = PEAK_F16_MFMA_TFLOPS / SPLIT_MFMA_PER_PRODUCT if mode == "split" else PEAK_FP32_MFMA_TFLOPS
+    return flops / (mfma_peak * 1e12), build_bytes / (PEAK_HBM_GBS * 1e9), mfma_peak
 
 
 def make_inputs(B, D, H, W, iters, device, seed):
@@ -371,14 +386,24 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, build_ms, look_ms = t.tolist()
 
-    flops, look_bytes = algorithmic(B, D, H, W, q=q_local)
+    flops, build_bytes, look_bytes = algorithmic(B, D, H, W, q=q_local)
+    mode = eraft_amd._lib.build_mode()
+    t_mfma, t_hbm, mfma_peak = build_floors(flops, build_bytes, mode)
     build_tf = flops / (build_ms * 1e-3) / 1e12
+    build_gbs = build_bytes / (build_ms * 1e-3) / 1e9
     look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
     note = "" if a.mode == "batch" else " (per rank; lookup time includes the output all-gather)"
+    mfma_roof = {"bound": "mfma", "achieved": round(build_tf, 2), "peak": round(mfma_peak, 1), "unit": "TFLOP/s",
+                 "frac": round(build_tf / mfma_peak, 4), "work_per_launch": f"{flops:.4g} flop" + note}
+    hbm_roof = {"bound": "hbm", "achieved": round(build_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(build_gbs / PEAK_HBM_GBS, 4),
+                "work_per_launch": f"{build_bytes:.4g} B (fmaps in + pyramid out)" + note}
+    # the build's binding roof is the one with the longer ideal time (fp32 MFMA: the matrix
+    # cores; split: HBM, the 1.96 GB pyramid store outweighs 3 f16 MFMAs per product)
+    bind, other = (mfma_roof, hbm_roof) if t_mfma >= t_hbm else (hbm_roof, mfma_roof)
     kernels = {
-        "build": {"bound": "mfma", "achieved": round(build_tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
-                  "unit": "TFLOP/s", "frac": round(build_tf / PEAK_FP32_MFMA_TFLOPS, 4),
-                  "ms_per_launch": round(build_ms, 4), "work_per_launch": f"{flops:.4g} flop" + note},
+        "build": dict(bind, ms_per_launch=round(build_ms, 4), mode=mode,
+                      other_roof={k: other[k] for k in ("bound", "achieved", "peak", "unit", "frac")}),
         "lookup": {"bound": "hbm", "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                    "frac": round(look_gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(look_ms, 4),
                    "launches_per_step": iters, "work_per_launch": f"{look_bytes:.4g} B" + note},
@@ -390,7 +415,7 @@ def main():
     roof["traffic"] = traffic
     if src:
         roof["traffic_source"] = src
-    ideal_s = flops / (PEAK_FP32_MFMA_TFLOPS * 1e12) + iters * look_bytes / (PEAK_HBM_GBS * 1e9)
+    ideal_s = max(t_mfma, t_hbm) + iters * look_bytes / (PEAK_HBM_GBS * 1e9)
     pairs = (world * B if a.mode == "batch" else B) * a.steps
     if a.mode == "batch":
         cfg = {"workload": f"DSEC 480x640 CorrBlock build + {iters} lookups, warm-start, batch {B} per GPU "
@@ -406,7 +431,7 @@ def main():
         "metric": METRIC, "value": round(pairs / elapsed, 2), "unit": "pairs/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak" if a.mode == "batch" else "strong",
-        "vs_baseline": None, "dtype": "fp32",
+        "vs_baseline": None, "dtype": "fp32" if mode == "fp32" else "fp32 (f16x3 split MFMA, fp32 accumulate)",
         "data": "synthetic (randn fmaps, coords_grid + smooth warm-start flow)",
         "config": cfg, "roofline": roof, "kernels": kernels,
         "corrblock_frac": round(ideal_s / (elapsed / a.steps), 4),

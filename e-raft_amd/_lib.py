@@ -36,8 +36,8 @@ SYMBOLS = {
                                   ctypes.POINTER(_i64)]),
     # (fmap1, fmap2, B, D, H, W, q_count, levels, pyramid, stream)
     "ecorr_build": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
-    # (B, H, W, q_count, bytes*)
-    "ecorr_build_split_workspace_size": (_i, [_i, _i, _i, _i, ctypes.POINTER(_i64)]),
+    # (B, D, H, W, q_count, bytes*)
+    "ecorr_build_split_workspace_size": (_i, [_i, _i, _i, _i, _i, ctypes.POINTER(_i64)]),
     # (fmap1, fmap2, B, D, H, W, q_count, levels, pyramid, workspace, stream)
     "ecorr_build_split": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     # (pyramid, coords, B, H, W, q_count, levels, radius, out, stream)
@@ -138,21 +138,21 @@ def build_mode() -> str:
 
 
 def build_pyramid(fmap1, fmap2, B, D, H, W, q_count, levels, off, what, mode=None):
-    """Allocate the pyramid (levels at off[i], plus the split build's exponent scratch as a tail
-    past off[-1]) on fmap2's device and build it on the current stream.  Returns the tensor."""
+    """Allocate the pyramid (levels at off[i]) on fmap2's device and build it on the current
+    stream.  The split build's workspace (exponents + packed f16 operand panels, about the fmaps'
+    size) is a temporary from the caching allocator, released stream-ordered after the launch."""
     mode = mode or _build_mode
     if mode not in BUILD_MODES:
         raise ValueError(f"build mode {mode!r} not in {BUILD_MODES}")
-    tail = 0
-    if mode == "split":
-        nbytes = _i64()
-        check(lib().ecorr_build_split_workspace_size(B, H, W, q_count, ctypes.byref(nbytes)), what)
-        tail = (nbytes.value + 127) // 128 * 32   # floats, whole 128-byte lines
-    pyr = torch.empty(off[-1] + tail, dtype=torch.float32, device=fmap2.device)
+    pyr = torch.empty(off[-1], dtype=torch.float32, device=fmap2.device)
     st = stream_of(fmap2)
     if mode == "split":
+        nbytes = _i64()
+        check(lib().ecorr_build_split_workspace_size(B, D, H, W, q_count, ctypes.byref(nbytes)), what)
+        ws = torch.empty(nbytes.value, dtype=torch.uint8, device=fmap2.device)
         check(lib().ecorr_build_split(fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, q_count, levels,
-                                      pyr.data_ptr(), pyr.data_ptr() + 4 * off[-1], st), what)
+                                      pyr.data_ptr(), ws.data_ptr(), st), what)
+        del ws
     else:
         check(lib().ecorr_build(fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, q_count, levels,
                                 pyr.data_ptr(), st), what)

@@ -122,9 +122,8 @@ int build_common(const float* fmap1, const float* fmap2, int B, int D, int H, in
     P.scale_is_mul = (mant == 0.5f) ? 1 : 0;
     P.scale = P.scale_is_mul ? 1.0f / s : s;
     if (workspace) {
-        if (B > 65535 || ((uintptr_t)workspace & 3)) return ECORR_EINVAL;
-        P.ex1 = static_cast<int*>(workspace);
-        P.ex2 = P.ex1 + (int64_t)B * q_count;
+        if (B > 65535 || ((uintptr_t)workspace & 255)) return ECORR_EINVAL;
+        P.ws = static_cast<char*>(workspace);
     }
     return launch_build(P, B, g, pyramid, (hipStream_t)stream);
 }
@@ -136,9 +135,9 @@ ECORR_EXPORT int ecorr_build(const float* fmap1, const float* fmap2, int B, int 
     return build_common(fmap1, fmap2, B, D, H, W, q_count, levels, pyramid, nullptr, stream);
 }
 
-ECORR_EXPORT int ecorr_build_split_workspace_size(int B, int H, int W, int q_count, int64_t* bytes) {
-    if (!bytes || B <= 0 || B > 65535 || !q_count_ok(H, W, q_count)) return ECORR_EINVAL;
-    *bytes = build_split_workspace_bytes(B, H, W, q_count);
+ECORR_EXPORT int ecorr_build_split_workspace_size(int B, int D, int H, int W, int q_count, int64_t* bytes) {
+    if (!bytes || B <= 0 || B > 65535 || D <= 0 || !q_count_ok(H, W, q_count)) return ECORR_EINVAL;
+    *bytes = build_split_workspace_bytes(B, D, H, W, q_count);
     return ECORR_OK;
 }
 

@@ -79,7 +79,7 @@ __device__ __forceinline__ float pool4(float a, float b, float c, float d) {
 // last 4 rows when H % 8 is 1..4, a 4 x 32 block ("band"): those rows feed pyramid levels 0-2 only
 // (level 3 of an H = 8k + r map, r <= 4, has k rows), so the band pools 4 x 8 sub-blocks and no
 // 8-row tile row is padded half empty (DSEC H = 60: 6.7% of the MFMA work saved).
-struct TileCoord { int b, m0, ty0, tx0, band; };
+struct TileCoord { int b, m0, ty0, tx0, band, mt, nt; };
 
 // Grouped tile order (8 m-tiles x all n-tiles per group): consecutive tiles share fmap panels.
 __device__ __forceinline__ TileCoord decode_tile(const BuildParams& P, int t) {
@@ -94,6 +94,8 @@ __device__ __forceinline__ TileCoord decode_tile(const BuildParams& P, int t) {
     const int gsm = min(P.n_mt - first_m, GM);
     const int mt = first_m + gi % gsm, nt = gi / gsm;
     c.m0 = mt * BM;
+    c.mt = mt;
+    c.nt = nt;
     if (nt < P.n_reg) {
         const int nty = nt / P.n_ntx, ntx = nt - nty * P.n_ntx;
         c.ty0 = nty * TBH;
@@ -354,8 +356,14 @@ __device__ __forceinline__ void wait_vmcnt() {
 // 3 x 32 vs 8 x 64 matrix-core cycles.  The fragment reads are the fp32 path's: lane (r, h) takes
 // k = 2j + h as element j, the same permutation on both operands.  Normwise error vs fp64 is
 // below the fp32 path's; the result is scaled back by 2^-(e1+e2) exactly.
-template <bool VEC, int KB, bool HALF, bool NTS, int GBUF = 0, bool SPLIT = false>
+//
+// PK (split mode, default): the operands arrive pre-split by pack_kernel as 8-KB panels (one per
+// 128-pixel tile and 16-deep K chunk) laid out in MFMA-fragment order, so LDS-DMA copies them
+// verbatim and each fragment is ONE lane-linear ds_read_b128: no VALU work in the K loop, no zero
+// fill (the panels carry their padding).
+template <bool VEC, int KB, bool HALF, bool NTS, int GBUF = 0, bool SPLIT = false, bool PK = false>
 __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) {
+    static_assert(!PK || (SPLIT && KB == 16 && GBUF > 0), "PK: split mode, 16-deep panels, LDS-DMA");
     constexpr int MR = HALF ? BM / 2 : BM;
     constexpr int AS = BM, BSS = BN;   // LDS row strides
     constexpr int NLD = (KB * BM / 4) / NT;   // float4 of A (and of B) per thread per chunk
@@ -453,7 +461,7 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
     const int nk = (D + KB - 1) / KB;
 
     float sa0 = 1.f, sa1 = 1.f, sb0 = 1.f, sb1 = 1.f;
-    if constexpr (SPLIT) {
+    if constexpr (SPLIT && !PK) {
         sa0 = exp2i(exs[wm * 64 + acol]);
         sa1 = exp2i(exs[wm * 64 + 32 + acol]);
         sb0 = exp2i(exs[BM + wn * 64 + acol]);
@@ -463,6 +471,32 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
     auto mfma_chunk = [&](int buf) {
         const float* as = As + buf * KB * AS + wm * 64 + acol;
         const float* bs = Bs + buf * KB * BSS + wn * 64 + acol;
+        if constexpr (PK) {
+            // panel: [32-row group][hi h0 | hi h1 | lo h0 | lo h1][32 rows][8 halves]
+            const char* ap = reinterpret_cast<const char*>(As + buf * KB * AS) + wm * 4096 + lane * 16;
+            const char* bp = reinterpret_cast<const char*>(Bs + buf * KB * BSS) + wn * 4096 + lane * 16;
+            const halfx8 a0h = *reinterpret_cast<const halfx8*>(ap);
+            const halfx8 a0l = *reinterpret_cast<const halfx8*>(ap + 1024);
+            const halfx8 a1h = *reinterpret_cast<const halfx8*>(ap + 2048);
+            const halfx8 a1l = *reinterpret_cast<const halfx8*>(ap + 3072);
+            const halfx8 b0h = *reinterpret_cast<const halfx8*>(bp);
+            const halfx8 b0l = *reinterpret_cast<const halfx8*>(bp + 1024);
+            const halfx8 b1h = *reinterpret_cast<const halfx8*>(bp + 2048);
+            const halfx8 b1l = *reinterpret_cast<const halfx8*>(bp + 3072);
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0l, b0h, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0l, b1h, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l, b0h, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l, b1h, acc[1][1], 0, 0, 0);
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b0l, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b1l, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b0l, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b1l, acc[1][1], 0, 0, 0);
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b0h, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b1h, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b0h, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b1h, acc[1][1], 0, 0, 0);
+            return;
+        }
         if constexpr (SPLIT) {
 #pragma unroll
             for (int k16 = 0; k16 < KB; k16 += 16) {
@@ -520,8 +554,29 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
         const int y = tc.ty0 + (tc.band ? c >> 3 : c >> 2), x = tc.tx0 + 4 * (tc.band ? c & 7 : c & 3);
         const bool aok = m < q_end, bok = y < H && x < W;
         const int abase = m * 4, bbase = (y * W + x) * 4;
+        // PK: this tile's panels, chunk-major (pack_kernel layout)
+        const int dc = (D + 15) / 16;
+        const char* pa = PK ? P.pk1 + ((int64_t)tc.b * P.n_mt + tc.mt) * dc * 8192 : nullptr;
+        const char* pb = PK ? P.pk2 + ((int64_t)tc.b * P.n_nt + tc.nt) * dc * 8192 : nullptr;
+        const __amdgpu_buffer_rsrc_t rpa =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pa), 0, dc * 8192, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rpb =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pb), 0, dc * 8192, 0x00020000);
         auto issue = [&](int kc) {
             const int buf = kc % NBUF;
+            if constexpr (PK) {
+#pragma unroll
+                for (int i = 0; i < NLD; ++i) {
+                    const int slot = i * NT + wave * 64;   // wave-uniform 16-byte slot of this copy
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rpa, (__attribute__((address_space(3))) void*)(As + buf * KB * AS + 4 * slot), 16,
+                        kc * 8192 + (slot + lane) * 16, 0, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rpb, (__attribute__((address_space(3))) void*)(Bs + buf * KB * BSS + 4 * slot), 16,
+                        kc * 8192 + (slot + lane) * 16, 0, 0, 0);
+                }
+                return;
+            }
 #pragma unroll
             for (int i = 0; i < NLD; ++i) {
                 const int kk = 2 * wave + 8 * i;   // wave-uniform first row of this copy
@@ -535,6 +590,69 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                     bok && kin ? bbase + k * (int)Q * 4 : OOB, 0, 0, 0);
             }
         };
+        if constexpr (PK) {
+            if (P.dev_pk_pipe && nk % 2 == 0) {
+                // software-pipelined (even chunk counts): chunk kc + 1's fragments are read (after
+                // its barrier) between the lo*hi MFMAs of chunk kc and its hi*lo / hi*hi MFMAs, so
+                // the barrier and the LDS latency hide behind the matrix pipe; two register sets,
+                // loop unrolled by 2
+                auto read_frags = [&](int buf, halfx8 (&f)[8]) {
+                    const char* ap = reinterpret_cast<const char*>(As + buf * KB * AS) + wm * 4096 + lane * 16;
+                    const char* bp = reinterpret_cast<const char*>(Bs + buf * KB * BSS) + wn * 4096 + lane * 16;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        f[q] = *reinterpret_cast<const halfx8*>(ap + q * 1024);       // a0h a0l a1h a1l
+                        f[4 + q] = *reinterpret_cast<const halfx8*>(bp + q * 1024);   // b0h b0l b1h b1l
+                    }
+                };
+                auto mfma_lohi = [&](const halfx8 (&f)[8]) {
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[1], f[4], acc[0][0], 0, 0, 0);
+                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[1], f[6], acc[0][1], 0, 0, 0);
+                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[3], f[4], acc[1][0], 0, 0, 0);
+                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[3], f[6], acc[1][1], 0, 0, 0);
+                };
+                auto mfma_rest = [&](const halfx8 (&f)[8]) {
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[0], f[5], acc[0][0], 0, 0, 0);
+                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[0], f[7], acc[0][1], 0, 0, 0);
+                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[2], f[5], acc[1][0], 0, 0, 0);
+                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[2], f[7], acc[1][1], 0, 0, 0);
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[0], f[4], acc[0][0], 0, 0, 0);
+                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[0], f[6], acc[0][1], 0, 0, 0);
+                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[2], f[4], acc[1][0], 0, 0, 0);
+                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[2], f[6], acc[1][1], 0, 0, 0);
+                };
+                // chunk j's buffer is j % NBUF; a chunk is issued into the buffer whose reads the
+                // preceding barrier retired.  Exactly one chunk stays in flight at every wait:
+                // chunks past the end are still issued (their offsets fall outside the panel range,
+                // so they land as zeros in a retired buffer) and the last advance reads such a
+                // chunk, which keeps the loop free of branches (and of conservative waitcnts)
+                auto advance = [&](int& issued, int j, halfx8 (&f)[8]) {
+                    // vmcnt(2 NLD (NBUF - 2)): chunk j landed, the NBUF - 2 after it may fly;
+                    // lgkmcnt(0): this wave's reads of chunk j - 1 (half of them not yet consumed
+                    // by an MFMA) are done before the barrier hands their buffer to chunk
+                    // j + NBUF - 1
+                    static_assert(2 * NLD * (NBUF - 2) < 16, "vmcnt field");
+                    __builtin_amdgcn_s_waitcnt((2 * NLD * (NBUF - 2)) | (7 << 4));
+                    __builtin_amdgcn_s_barrier();
+                    issue(issued++);
+                    read_frags(j % NBUF, f);
+                };
+                halfx8 fa[8], fb[8];
+                int issued = 0;
+                while (issued < NBUF - 1) issue(issued++);
+                advance(issued, 0, fa);
+                for (int kc = 0; kc < nk; kc += 2) {
+                    mfma_lohi(fa);
+                    advance(issued, kc + 1, fb);
+                    mfma_rest(fa);
+                    mfma_lohi(fb);
+                    advance(issued, kc + 2, fa);
+                    mfma_rest(fb);
+                }
+                wait_vmcnt<0>();
+                goto chunks_done;
+            }
+        }
         for (int kc = 0; kc < NBUF - 1 && kc < nk; ++kc) issue(kc);
         for (int kc = 0; kc < nk; ++kc) {
             // this wave's copies of chunk kc have landed (those of the later issued chunks may
@@ -554,6 +672,7 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
             if (kc + NBUF - 1 < nk && P.dev_skip_epilogue < 3) issue(kc + NBUF - 1);
             mfma_chunk(kc % NBUF);
         }
+    chunks_done:
         __syncthreads();   // the C tile aliases the chunk buffers
     } else {
         load_chunk(0);
@@ -641,16 +760,100 @@ __global__ __launch_bounds__(256) void fmap_exp_kernel(const float* __restrict__
     }
 }
 
-}  // namespace
-
-int64_t build_split_workspace_bytes(int B, int H, int W, int q_count) {
-    return ((int64_t)B * q_count + (int64_t)B * H * W) * (int64_t)sizeof(int);
+// Split-mode operand pass (PK build): per pixel, the power-of-two exponent of fmap_exp_kernel and
+// the f16 hi/lo split of all D values, written as the build's 8-KB panels: panel (tile, chunk) =
+// [32-row group g][hi k0-7 | hi k8-15 | lo k0-7 | lo k8-15][row r][8 halves], i.e. the
+// v_mfma_f32_32x32x16_f16 operand of lane (r, h) is the 16 bytes at g*2048 + part*1024 + lane*16.
+// Tile positions without a pixel (ragged edges) and k >= D are written as zeros.
+// ISB = 0: fmap1 slab, tile = 128 consecutive queries; ISB = 1: fmap2, tile = the build's 8 x 16
+// (or 4 x 32 band) target block in its LDS column order.  Block = 64 positions x 4 chunk
+// quarters; grid (2 * tiles, B).  The second pass re-reads the block's 64 KB (L2 / MALL hits).
+template <bool ISB>
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, BuildParams P, int* __restrict__ ex,
+                                                   char* __restrict__ pack) {
+    __shared__ float red[4][64];
+    const int b = blockIdx.y, tile = blockIdx.x >> 1, pos = (blockIdx.x & 1) * 64 + (threadIdx.x & 63);
+    const int qtr = threadIdx.x >> 6, D = P.D, dc = (D + 15) / 16;
+    const int64_t N = ISB ? (int64_t)P.H * P.W : (int64_t)P.q_count;
+    int64_t pix = -1;
+    if (!ISB) {
+        const int64_t p = (int64_t)tile * BM + pos;
+        if (p < P.q_count) pix = p;
+    } else {
+        int y, xx;
+        if (tile < P.n_reg) {
+            y = (tile / P.n_ntx) * TBH + (pos >> 4);
+            xx = (tile % P.n_ntx) * TBW + (pos & 15);
+        } else {
+            y = P.band_y0 + (pos >> 5);
+            xx = (tile - P.n_reg) * 32 + (pos & 31);
+        }
+        if (y < P.H && xx < P.W) pix = (int64_t)y * P.W + xx;
+    }
+    const float* px = x + (int64_t)b * D * N + (pix < 0 ? 0 : pix);
+    // D <= 256 (E-RAFT: 256): this thread's <= 4 chunks stay in registers between the max and the
+    // split, so the operand is read once; larger D re-reads it in the second pass
+    constexpr int CPT = 4;
+    const bool regs = dc <= 4 * CPT;
+    float v[CPT][16];
+    float m = 0.f;
+    if (regs) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) {
+                const int k = (qtr + 4 * i) * 16 + kk;
+                v[i][kk] = (pix >= 0 && k < D) ? px[(int64_t)k * N] : 0.f;
+                m = fmaxf(m, fabsf(v[i][kk]));
+            }
+    } else if (pix >= 0) {
+        for (int k = qtr * 16; k < D; k += 64)
+#pragma unroll 4
+            for (int kk = 0; kk < 16 && k + kk < D; ++kk) m = fmaxf(m, fabsf(px[(int64_t)(k + kk) * N]));
+    }
+    red[qtr][threadIdx.x & 63] = m;
+    __syncthreads();
+    const int l = threadIdx.x & 63;
+    m = fmaxf(fmaxf(red[0][l], red[1][l]), fmaxf(red[2][l], red[3][l]));
+    int E = 0;
+    frexpf(m, &E);
+    int e = (m > 0.f && m <= 3.4028235e38f) ? 15 - E : 0;
+    e = e < -126 ? -126 : (e > 126 ? 126 : e);
+    if (qtr == 0 && pix >= 0) ex[(int64_t)b * N + pix] = e;
+    const float s = exp2i(e);
+    const int ntiles = ISB ? P.n_nt : P.n_mt;
+    char* pan = pack + ((int64_t)b * ntiles + tile) * dc * 8192 + (pos >> 5) * 2048 + (pos & 31) * 16;
+    auto put = [&](int c, const float (&w)[16]) {
+        halfx8 h0, l0, h1, l1;
+        split_f16(*reinterpret_cast<const float(*)[8]>(w), s, h0, l0);
+        split_f16(*reinterpret_cast<const float(*)[8]>(w + 8), s, h1, l1);
+        char* p = pan + (int64_t)c * 8192;
+        *reinterpret_cast<halfx8*>(p) = h0;
+        *reinterpret_cast<halfx8*>(p + 512) = h1;
+        *reinterpret_cast<halfx8*>(p + 1024) = l0;
+        *reinterpret_cast<halfx8*>(p + 1536) = l1;
+    };
+    if (regs) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i)
+            if (qtr + 4 * i < dc) put(qtr + 4 * i, v[i]);
+        return;
+    }
+    for (int c = qtr; c < dc; c += 4) {
+        float w[16];
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+            const int k = c * 16 + kk;
+            w[kk] = (pix >= 0 && k < D) ? px[(int64_t)k * N] : 0.f;
+        }
+        put(c, w);
+    }
 }
 
-int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid, hipStream_t stream) {
-    BuildParams P = P0;
-    const int levels = g.levels;
-    P.fused_levels = levels < 4 ? levels : 4;
+}  // namespace
+
+namespace {
+void tile_counts(BuildParams& P) {
     P.n_ntx = (P.W + TBW - 1) / TBW;
     // 8-row tile rows; a remainder of 1..4 rows (the last 8k + r rows, r <= 4) becomes a band of
     // 4 x 32 tiles (see TileCoord), a remainder of 5..7 a padded regular tile row
@@ -661,6 +864,36 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
     P.band_y0 = (P.H / TBH) * TBH;
     P.n_nt = P.n_reg + (band ? (P.W + 31) / 32 : 0);
     P.n_mt = (P.q_count + BM - 1) / BM;
+}
+
+// split workspace: exponents (fmap1 slab, fmap2), then fmap1 and fmap2 panels (256-B aligned)
+struct SplitWs { int64_t ex2, pk1, pk2, total; };
+SplitWs split_ws(const BuildParams& P, int B) {
+    const int64_t dc = (P.D + 15) / 16;
+    SplitWs w;
+    w.ex2 = (int64_t)B * P.q_count * 4;
+    w.pk1 = (w.ex2 + (int64_t)B * P.H * P.W * 4 + 255) & ~(int64_t)255;
+    w.pk2 = w.pk1 + (int64_t)B * P.n_mt * dc * 8192;
+    w.total = w.pk2 + (int64_t)B * P.n_nt * dc * 8192;
+    return w;
+}
+}  // namespace
+
+int64_t build_split_workspace_bytes(int B, int D, int H, int W, int q_count) {
+    BuildParams P{};
+    P.D = D;
+    P.H = H;
+    P.W = W;
+    P.q_count = q_count;
+    tile_counts(P);
+    return split_ws(P, B).total;
+}
+
+int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid, hipStream_t stream) {
+    BuildParams P = P0;
+    const int levels = g.levels;
+    P.fused_levels = levels < 4 ? levels : 4;
+    tile_counts(P);
     for (int i = 0; i < 4; ++i) {
         const bool on = i < levels;
         P.lvl[i] = on ? pyramid + g.off[i] : nullptr;
@@ -693,13 +926,35 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
     const bool glds = !(kg && atoi(kg) == 0) && (int64_t)P.D * P.H * P.W * 4 < 0x7fff0000LL &&
                       (int64_t)P.D * P.q_count * 4 < 0x7fff0000LL;
     const dim3 grid((unsigned)ntiles), block(NT);
-    if (P.ex1) {
+    if (P.ws) {
         const int64_t Q = (int64_t)P.H * P.W;
-        hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((P.q_count + 63) / 64), B), dim3(256), 0, stream, P.f1,
-                           P.D, (int64_t)P.q_count, P.ex1);
-        hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((Q + 63) / 64), B), dim3(256), 0, stream, P.f2, P.D, Q,
-                           P.ex2);
-        if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true, 0, true>), grid, block, 0, stream, P);
+        const SplitWs w = split_ws(P, B);
+        P.ex1 = reinterpret_cast<int*>(P.ws);
+        P.ex2 = reinterpret_cast<int*>(P.ws + w.ex2);
+        P.pk1 = P.ws + w.pk1;
+        P.pk2 = P.ws + w.pk2;
+        // PK needs one batch item's panels inside the 31-bit buffer range; dev knob
+        // ECORR_BUILD_PK=0 selects the in-loop split (A/B)
+        const char* kp = getenv("ECORR_BUILD_PK");
+        const char* kpp = getenv("ECORR_BUILD_PKPIPE");   // dev knob: 0 = unpipelined PK loop (A/B)
+        P.dev_pk_pipe = !(kpp && atoi(kpp) == 0);
+        const bool pk = !(kp && atoi(kp) == 0) &&
+                        (int64_t)(P.n_mt > P.n_nt ? P.n_mt : P.n_nt) * ((P.D + 15) / 16) * 8192 < 0x7fff0000LL;
+        if (pk) {
+            hipLaunchKernelGGL(pack_kernel<false>, dim3((unsigned)(2 * P.n_mt), B), dim3(256), 0, stream, P.f1, P,
+                               P.ex1, P.ws + w.pk1);
+            hipLaunchKernelGGL(pack_kernel<true>, dim3((unsigned)(2 * P.n_nt), B), dim3(256), 0, stream, P.f2, P,
+                               P.ex2, P.ws + w.pk2);
+            hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true>), grid, block, 0, stream, P);
+        } else {
+            hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((P.q_count + 63) / 64), B), dim3(256), 0, stream,
+                               P.f1, P.D, (int64_t)P.q_count, P.ex1);
+            hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((Q + 63) / 64), B), dim3(256), 0, stream, P.f2, P.D,
+                               Q, P.ex2);
+        }
+        if (pk) {
+            // launched above
+        } else if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true, 0, true>), grid, block, 0, stream, P);
         else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true>), grid, block, 0, stream, P);
         else hipLaunchKernelGGL((build_kernel<true, 16, true, true, 0, true>), grid, block, 0, stream, P);
     } else if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true>), grid, block, 0, stream, P);

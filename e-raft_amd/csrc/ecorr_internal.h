@@ -29,8 +29,12 @@ struct BuildParams {
     int scale_is_mul;
     // split mode (ecorr_build_split): per-pixel power-of-two exponents of fmap1 ([B][q_count]) and
     // fmap2 ([B][H*W]) written by the exponent pass; null = the fp32-MFMA fmaf-chain build
+    char* ws;           // split workspace (build_split_workspace_bytes), null = fp32 build
     int* ex1;
     int* ex2;
+    const char* pk1;    // PK panels of fmap1 / fmap2 (pack_kernel)
+    const char* pk2;
+    int dev_pk_pipe;    // software-pipelined PK loop (default 1; ECORR_BUILD_PKPIPE=0 for A/B)
     // filled by launch_build
     int n_mt, n_nt, n_ntx, n_tiles;
     int n_reg, band_y0;  // regular (8 x 16) n-tiles per m-tile; first row of the 4-row band tiles
@@ -43,7 +47,7 @@ struct BuildParams {
 };
 
 int launch_build(const BuildParams& P, int B, const PyrGeom& g, float* pyramid, hipStream_t stream);
-int64_t build_split_workspace_bytes(int B, int H, int W, int q_count);
+int64_t build_split_workspace_bytes(int B, int D, int H, int W, int q_count);
 
 struct LookupParams {
     const float* coords;  // [B][2][q_count]

@@ -69,10 +69,11 @@ int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int
  * operand is scaled by a per-pixel power of two and split into f16 hi + lo, and every product is
  * summed as lo*hi + hi*lo + hi*hi in fp32 -- error vs fp64 below the fp32-MFMA path's.  Per-pixel
  * scales depend only on that pixel's D values, so row-sharded and whole builds agree bit for bit.
- * workspace: ecorr_build_split_workspace_size() bytes of device memory (4-byte aligned, scratch
- * for the exponents; free after the call completes on `stream`).  B <= 65535.
+ * workspace: ecorr_build_split_workspace_size() bytes of device memory, 256-byte aligned (the
+ * exponents and the pre-split operands in MFMA-fragment order, about the two fmaps' size; free
+ * once the call has completed on `stream`).  B <= 65535.
  * Replaces: CorrBlock.__init__ (corr.py:13-27) and CorrBlock.corr (corr.py:52-60). */
-int ecorr_build_split_workspace_size(int B, int H, int W, int q_count, int64_t* bytes);
+int ecorr_build_split_workspace_size(int B, int D, int H, int W, int q_count, int64_t* bytes);
 int ecorr_build_split(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
                       int levels, float* pyramid, void* workspace, void* stream);
 

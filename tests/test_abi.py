@@ -122,12 +122,16 @@ def test_split_build_arguments(ea):
     from eraft_amd import _lib
     L = _lib.lib()
     n = ctypes.c_int64()
-    assert L.ecorr_build_split_workspace_size(16, 60, 80, 4800, ctypes.byref(n)) == 0
-    assert n.value == 4 * (16 * 4800 + 16 * 4800)
-    assert L.ecorr_build_split_workspace_size(4, 92, 160, 1840, ctypes.byref(n)) == 0
-    assert n.value == 4 * (4 * 1840 + 4 * 92 * 160)
-    assert L.ecorr_build_split_workspace_size(0, 60, 80, 4800, ctypes.byref(n)) == _lib.ECORR_EINVAL
-    assert L.ecorr_build_split_workspace_size(1, 60, 80, 4801, ctypes.byref(n)) == _lib.ECORR_EINVAL
+    # exponents (2 x B x 4800 ints, 256-B aligned) + 8-KB f16 hi/lo panels per (tile, 16-deep chunk):
+    # 38 query tiles and 38 target tiles (35 8x16 blocks + 3 4x32 band blocks) at 60 x 80
+    assert L.ecorr_build_split_workspace_size(16, 256, 60, 80, 4800, ctypes.byref(n)) == 0
+    assert n.value == 2 * 16 * 4800 * 4 + 2 * 16 * 38 * 16 * 8192
+    # query slab of 20 rows x 160 of a 92 x 160 map: 25 query tiles; 11 x 10 + 5 band target tiles
+    assert L.ecorr_build_split_workspace_size(4, 256, 92, 160, 3200, ctypes.byref(n)) == 0
+    ex = (4 * 3200 * 4 + 4 * 92 * 160 * 4 + 255) // 256 * 256
+    assert n.value == ex + 4 * 25 * 16 * 8192 + 4 * 115 * 16 * 8192
+    assert L.ecorr_build_split_workspace_size(0, 256, 60, 80, 4800, ctypes.byref(n)) == _lib.ECORR_EINVAL
+    assert L.ecorr_build_split_workspace_size(1, 256, 60, 80, 4801, ctypes.byref(n)) == _lib.ECORR_EINVAL
     assert L.ecorr_build_split(8, 8, 1, 256, 8, 8, 64, 4, 8, None, None) == _lib.ECORR_EINVAL
     with pytest.raises(ValueError):
         _lib.set_build_mode("bf16")

@@ -15,7 +15,13 @@ VARIANTS = {
     "default": {},
     "regstage": {"ECORR_BUILD_GLDS": "0"},
 }
-KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32", "ECORR_BUILD_NOBAND", "ECORR_BUILD_GLDS")
+# AB_VARIANTS='{"name": {"KNOB": "v", ...}, ...}' overrides; the pseudo-knob MODE picks the build
+# mode (_lib.set_build_mode), the rest are the launch_build env knobs below
+if os.environ.get("AB_VARIANTS"):
+    import json
+    VARIANTS = json.loads(os.environ["AB_VARIANTS"])
+KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32", "ECORR_BUILD_NOBAND", "ECORR_BUILD_GLDS",
+         "ECORR_BUILD_PK", "ECORR_BUILD_PKPIPE")
 B = int(os.environ.get("AB_BATCH", "16"))
 H, W, D = 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)
@@ -29,13 +35,14 @@ with torch.no_grad():
     for rnd in range(int(os.environ.get("AB_ROUNDS", "8"))):
         # rotate the order every round: the first variant of a round runs measurably slower
         for name in names[rnd % len(names):] + names[:rnd % len(names)]:
-            env = VARIANTS[name]
+            env = dict(VARIANTS[name])
+            eraft_amd._lib.set_build_mode(env.pop("MODE", "split"))
             for k in KNOBS:
                 os.environ.pop(k, None)
             os.environ.update(env)
             blk = eraft_amd.CorrBlock(f1, f2)   # warm
             torch.cuda.synchronize()
-            if rnd == 0 and "noepi" not in name and "nol0" not in name and "nnn" not in name:   # every variant must produce a valid pyramid (pooling exact vs level 0)
+            if rnd == 0 and "ECORR_BUILD_SKIP_EPILOGUE" not in VARIANTS[name]:   # every variant must produce a valid pyramid (pooling exact vs level 0)
                 blk._levels_cache = None
                 lv0, lv1 = blk.corr_pyramid[0][:64, 0], blk.corr_pyramid[1][:64, 0]
                 p = (((lv0[:, 0::2, 0::2] + lv0[:, 0::2, 1::2]) + lv0[:, 1::2, 0::2]) + lv0[:, 1::2, 1::2]) * 0.25
