@@ -83,7 +83,7 @@ struct TileCoord { int b, m0, ty0, tx0, band, mt, nt; };
 
 // Grouped tile order (8 m-tiles x all n-tiles per group): consecutive tiles share fmap panels.
 __device__ __forceinline__ TileCoord decode_tile(const BuildParams& P, int t) {
-    constexpr int GM = 8;
+    const int GM = P.gm;
     const int per_b = P.n_mt * P.n_nt;
     TileCoord c;
     c.b = t / per_b;
@@ -894,6 +894,9 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
     const int levels = g.levels;
     P.fused_levels = levels < 4 ? levels : 4;
     tile_counts(P);
+    // m-tiles per group of the tile order (dev knob ECORR_BUILD_GM for A/B; default 8)
+    const char* kgm = getenv("ECORR_BUILD_GM");
+    P.gm = kgm && atoi(kgm) > 0 ? atoi(kgm) : 8;
     for (int i = 0; i < 4; ++i) {
         const bool on = i < levels;
         P.lvl[i] = on ? pyramid + g.off[i] : nullptr;

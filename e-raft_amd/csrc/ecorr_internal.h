@@ -34,7 +34,8 @@ struct BuildParams {
     int* ex2;
     const char* pk1;    // PK panels of fmap1 / fmap2 (pack_kernel)
     const char* pk2;
-    int dev_pk_pipe;    // software-pipelined PK loop (default 1; ECORR_BUILD_PKPIPE=0 for A/B)
+    int dev_pk_pipe;
+    int gm;             // m-tiles per group of the grouped tile order    // software-pipelined PK loop (default 1; ECORR_BUILD_PKPIPE=0 for A/B)
     // filled by launch_build
     int n_mt, n_nt, n_ntx, n_tiles;
     int n_reg, band_y0;  // regular (8 x 16) n-tiles per m-tile; first row of the 4-row band tiles
