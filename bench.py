@@ -403,6 +403,8 @@ def main():
     bind, other = (mfma_roof, hbm_roof) if t_mfma >= t_hbm else (hbm_roof, mfma_roof)
     kernels = {
         "build": dict(bind, ms_per_launch=round(build_ms, 4), mode=mode,
+                      covers=("pack_kernel<false> + pack_kernel<true> + build_kernel (one CorrBlock build; "
+                              "HIP events on the launch stream)") if mode == "split" else "build_kernel",
                       other_roof={k: other[k] for k in ("bound", "achieved", "peak", "unit", "frac")}),
         "lookup": {"bound": "hbm", "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                    "frac": round(look_gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(look_ms, 4),
