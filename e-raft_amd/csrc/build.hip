@@ -361,7 +361,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 // 128-pixel tile and 16-deep K chunk) laid out in MFMA-fragment order, so LDS-DMA copies them
 // verbatim and each fragment is ONE lane-linear ds_read_b128: no VALU work in the K loop, no zero
 // fill (the panels carry their padding).
-template <bool VEC, int KB, bool HALF, bool NTS, int GBUF = 0, bool SPLIT = false, bool PK = false>
+// ABL (A/B ablation of the pipelined PK loop only, output invalid; ECORR_BUILD_ABL): 5 no MFMA,
+// 6 no fragment reads, 7 no barrier, 8 no chunk copies -- each also without the epilogue.
+template <bool VEC, int KB, bool HALF, bool NTS, int GBUF = 0, bool SPLIT = false, bool PK = false, int ABL = 0>
 __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) {
     static_assert(!PK || (SPLIT && KB == 16 && GBUF > 0), "PK: split mode, 16-deep panels, LDS-DMA");
     constexpr int MR = HALF ? BM / 2 : BM;
@@ -597,6 +599,7 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                 // the barrier and the LDS latency hide behind the matrix pipe; two register sets,
                 // loop unrolled by 2
                 auto read_frags = [&](int buf, halfx8 (&f)[8]) {
+                    if constexpr (ABL == 6) return;
                     const char* ap = reinterpret_cast<const char*>(As + buf * KB * AS) + wm * 4096 + lane * 16;
                     const char* bp = reinterpret_cast<const char*>(Bs + buf * KB * BSS) + wn * 4096 + lane * 16;
 #pragma unroll
@@ -606,12 +609,18 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                     }
                 };
                 auto mfma_lohi = [&](const halfx8 (&f)[8]) {
+                    if constexpr (ABL == 5) {
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) asm volatile("" ::"v"(f[q]));
+                        return;
+                    }
                     acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[1], f[4], acc[0][0], 0, 0, 0);
                     acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[1], f[6], acc[0][1], 0, 0, 0);
                     acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[3], f[4], acc[1][0], 0, 0, 0);
                     acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[3], f[6], acc[1][1], 0, 0, 0);
                 };
                 auto mfma_rest = [&](const halfx8 (&f)[8]) {
+                    if constexpr (ABL == 5) return;
                     acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[0], f[5], acc[0][0], 0, 0, 0);
                     acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[0], f[7], acc[0][1], 0, 0, 0);
                     acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[2], f[5], acc[1][0], 0, 0, 0);
@@ -633,11 +642,16 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                     // j + NBUF - 1
                     static_assert(2 * NLD * (NBUF - 2) < 16, "vmcnt field");
                     __builtin_amdgcn_s_waitcnt((2 * NLD * (NBUF - 2)) | (7 << 4));
-                    __builtin_amdgcn_s_barrier();
-                    issue(issued++);
+                    if constexpr (ABL != 7) __builtin_amdgcn_s_barrier();
+                    if constexpr (ABL != 8) issue(issued);
+                    ++issued;
                     read_frags(j % NBUF, f);
                 };
                 halfx8 fa[8], fb[8];
+                if constexpr (ABL == 6) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) fa[q] = fb[q] = halfx8{};
+                }
                 int issued = 0;
                 while (issued < NBUF - 1) issue(issued++);
                 advance(issued, 0, fa);
@@ -709,7 +723,7 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                     }
         }
         __syncthreads();
-        if (P.dev_skip_epilogue == 1 || P.dev_skip_epilogue >= 3) continue;
+        if (ABL || P.dev_skip_epilogue == 1 || P.dev_skip_epilogue >= 3) continue;
         if (tc.band) epilogue_band<MR, NTS>(P, tc, Cs, tid, half * MR);
         else epilogue<MR, NTS>(P, tc, Cs, tid, half * MR);
         if (HALF && half == 0) __syncthreads();   // half 0 fully consumed before half 1 overwrites Cs
@@ -948,7 +962,14 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
                                P.ex1, P.ws + w.pk1);
             hipLaunchKernelGGL(pack_kernel<true>, dim3((unsigned)(2 * P.n_nt), B), dim3(256), 0, stream, P.f2, P,
                                P.ex2, P.ws + w.pk2);
-            hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true>), grid, block, 0, stream, P);
+            const char* ka = getenv("ECORR_BUILD_ABL");   // dev knob: loop ablations (A/B only)
+            switch (ka && P.dev_pk_pipe ? atoi(ka) : 0) {
+                case 5: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true, 5>), grid, block, 0, stream, P); break;
+                case 6: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true, 6>), grid, block, 0, stream, P); break;
+                case 7: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true, 7>), grid, block, 0, stream, P); break;
+                case 8: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true, 8>), grid, block, 0, stream, P); break;
+                default: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true>), grid, block, 0, stream, P);
+            }
         } else {
             hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((P.q_count + 63) / 64), B), dim3(256), 0, stream,
                                P.f1, P.D, (int64_t)P.q_count, P.ex1);

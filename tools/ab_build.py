@@ -21,7 +21,7 @@ if os.environ.get("AB_VARIANTS"):
     import json
     VARIANTS = json.loads(os.environ["AB_VARIANTS"])
 KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32", "ECORR_BUILD_NOBAND", "ECORR_BUILD_GLDS",
-         "ECORR_BUILD_PK", "ECORR_BUILD_PKPIPE", "ECORR_BUILD_GM")
+         "ECORR_BUILD_PK", "ECORR_BUILD_PKPIPE", "ECORR_BUILD_GM", "ECORR_BUILD_ABL")
 B = int(os.environ.get("AB_BATCH", "16"))
 H, W, D = 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)
@@ -42,7 +42,7 @@ with torch.no_grad():
             os.environ.update(env)
             blk = eraft_amd.CorrBlock(f1, f2)   # warm
             torch.cuda.synchronize()
-            if rnd == 0 and "ECORR_BUILD_SKIP_EPILOGUE" not in VARIANTS[name]:   # every variant must produce a valid pyramid (pooling exact vs level 0)
+            if rnd == 0 and not {"ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_ABL"} & set(VARIANTS[name]):   # every variant must produce a valid pyramid (pooling exact vs level 0)
                 blk._levels_cache = None
                 lv0, lv1 = blk.corr_pyramid[0][:64, 0], blk.corr_pyramid[1][:64, 0]
                 p = (((lv0[:, 0::2, 0::2] + lv0[:, 0::2, 1::2]) + lv0[:, 1::2, 0::2]) + lv0[:, 1::2, 1::2]) * 0.25
