@@ -43,13 +43,16 @@ with torch.no_grad():
     bias = torch.randn((256,), generator=g, device="cuda") * 0.1
     fused = hasattr(blk, "lookup_conv1x1_relu")
     algo = B * H * W * 2904
-    times = {(k, op): [] for k in LIBS for op in ("lookup", "fused")}
+    # integer coordinates (zero flow: the first iteration without warm start) exercise the
+    # floor-flip cases of the normalize/unnormalize round trip
+    coords_int = [base.contiguous() for _ in range(12)]
+    times = {(k, op): [] for k in LIBS for op in ("lookup", "lookup_int", "fused")}
     ref = {}
     names = list(LIBS)
     for rnd in range(int(os.environ.get("AB_ROUNDS", "8"))):
         for name in names[rnd % 2:] + names[:rnd % 2]:
             _lib._lib = LIBS[name]
-            outs = {"lookup": blk(coords[0])}
+            outs = {"lookup": blk(coords[0]), "lookup_int": blk(coords_int[0])}
             if fused:
                 outs["fused"] = blk.lookup_conv1x1_relu(coords[0], wt, bias)
             torch.cuda.synchronize()
@@ -62,8 +65,8 @@ with torch.no_grad():
             for op in outs:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for c in coords:
-                    blk(c) if op == "lookup" else blk.lookup_conv1x1_relu(c, wt, bias)
+                for c in (coords_int if op == "lookup_int" else coords):
+                    blk(c) if op.startswith("lookup") else blk.lookup_conv1x1_relu(c, wt, bias)
                 e1.record()
                 torch.cuda.synchronize()
                 times[(name, op)].append(e0.elapsed_time(e1) / len(coords))
@@ -71,5 +74,5 @@ for (name, op), ts in times.items():
     if not ts:
         continue
     med = statistics.median(ts)
-    extra = f"  -> {algo / med / 1e6:.0f} GB/s algorithmic" if op == "lookup" else ""
-    print(f"{op:6s} {name:5s} median {med * 1e3:.1f} us/call  min {min(ts) * 1e3:.1f}{extra}")
+    extra = f"  -> {algo / med / 1e6:.0f} GB/s algorithmic" if op.startswith("lookup") else ""
+    print(f"{op:10s} {name:5s} median {med * 1e3:.1f} us/call  min {min(ts) * 1e3:.1f}{extra}")
