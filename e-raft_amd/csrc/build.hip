@@ -970,17 +970,15 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
                 case 8: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true, 8>), grid, block, 0, stream, P); break;
                 default: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true>), grid, block, 0, stream, P);
             }
-        } else {
+        } else {   // in-loop split: exponents only, fp32 operands staged as in the fp32 build
             hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((P.q_count + 63) / 64), B), dim3(256), 0, stream,
                                P.f1, P.D, (int64_t)P.q_count, P.ex1);
             hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((Q + 63) / 64), B), dim3(256), 0, stream, P.f2, P.D,
                                Q, P.ex2);
+            if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true, 0, true>), grid, block, 0, stream, P);
+            else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true>), grid, block, 0, stream, P);
+            else hipLaunchKernelGGL((build_kernel<true, 16, true, true, 0, true>), grid, block, 0, stream, P);
         }
-        if (pk) {
-            // launched above
-        } else if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true, 0, true>), grid, block, 0, stream, P);
-        else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true>), grid, block, 0, stream, P);
-        else hipLaunchKernelGGL((build_kernel<true, 16, true, true, 0, true>), grid, block, 0, stream, P);
     } else if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true>), grid, block, 0, stream, P);
     else if (kb32) hipLaunchKernelGGL((build_kernel<true, 32, false, true>), grid, block, 0, stream, P);
     else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3>), grid, block, 0, stream, P);
