@@ -121,6 +121,7 @@ int build_common(const float* fmap1, const float* fmap2, int B, int D, int H, in
     const float mant = frexpf(s, &e);
     P.scale_is_mul = (mant == 0.5f) ? 1 : 0;
     P.scale = P.scale_is_mul ? 1.0f / s : s;
+    P.scale_shift = P.scale_is_mul ? e - 1 : 0;   // s = 0.5 * 2^e
     if (workspace) {
         if (B > 65535 || ((uintptr_t)workspace & 255)) return ECORR_EINVAL;
         P.ws = static_cast<char*>(workspace);

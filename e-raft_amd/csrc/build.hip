@@ -708,19 +708,31 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
     for (int half = 0; half < (HALF ? 2 : 1); ++half) {
         if (!HALF || wm == half) {
             const int mb = HALF ? 0 : wm * 64;
+            // one uniform branch on the scale mode around the whole tile (a per-element select
+            // had the compiler emit an IEEE division next to every element's multiply)
+            auto write_c = [&](auto scaled) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+                    for (int j = 0; j < 2; ++j)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int m = mb + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
-                        const int n = wn * 64 + j * 32 + acol;
-                        float v = acc[i][j][r];
-                        // SPLIT: undo the 2^(e1+e2) operand scaling (exact unless subnormal)
-                        if constexpr (SPLIT) v = ldexpf(v, -(exs[(HALF ? half * 64 : 0) + m] + exs[BM + n]));
-                        Cs[m * CS + n] = P.scale_is_mul ? __fmul_rn(v, P.scale) : __fdiv_rn(v, P.scale);
-                    }
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = mb + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
+                            const int n = wn * 64 + j * 32 + acol;
+                            const int e = SPLIT ? exs[(HALF ? half * 64 : 0) + m] + exs[BM + n] : 0;
+                            Cs[m * CS + n] = scaled(acc[i][j][r], e);
+                        }
+            };
+            if (P.scale_is_mul) {
+                // v * 2^-(e1+e2) * 2^-s as one exact scaling (unless subnormal) when 1/sqrt(D) = 2^-s
+                if constexpr (SPLIT) write_c([&](float v, int e) { return ldexpf(v, -(e + P.scale_shift)); });
+                else write_c([&](float v, int) { return __fmul_rn(v, P.scale); });
+            } else {
+                write_c([&](float v, int e) {
+                    // SPLIT: undo the 2^(e1+e2) operand scaling (exact unless subnormal), then divide
+                    return __fdiv_rn(SPLIT ? ldexpf(v, -e) : v, P.scale);
+                });
+            }
         }
         __syncthreads();
         if (ABL || P.dev_skip_epilogue == 1 || P.dev_skip_epilogue >= 3) continue;

@@ -27,6 +27,7 @@ struct BuildParams {
     int q_count;        // query pixels in the fmap1 slab
     float scale;        // sqrt(D) (divide) or 1/sqrt(D) when sqrt(D) is a power of two (multiply)
     int scale_is_mul;
+    int scale_shift;    // scale_is_mul: 1/sqrt(D) = 2^-scale_shift
     // split mode (ecorr_build_split): per-pixel power-of-two exponents of fmap1 ([B][q_count]) and
     // fmap2 ([B][H*W]) written by the exponent pass; null = the fp32-MFMA fmaf-chain build
     char* ws;           // split workspace (build_split_workspace_bytes), null = fp32 build

@@ -46,13 +46,14 @@ with torch.no_grad():
     # integer coordinates (zero flow: the first iteration without warm start) exercise the
     # floor-flip cases of the normalize/unnormalize round trip
     coords_int = [base.contiguous() for _ in range(12)]
-    times = {(k, op): [] for k in LIBS for op in ("lookup", "lookup_int", "fused")}
+    times = {(k, op): [] for k in LIBS for op in ("build", "lookup", "lookup_int", "fused")}
     ref = {}
     names = list(LIBS)
     for rnd in range(int(os.environ.get("AB_ROUNDS", "8"))):
         for name in names[rnd % 2:] + names[:rnd % 2]:
             _lib._lib = LIBS[name]
-            outs = {"lookup": blk(coords[0]), "lookup_int": blk(coords_int[0])}
+            outs = {"build": eraft_amd.CorrBlock(f1, f2)._pyramid, "lookup": blk(coords[0]),
+                    "lookup_int": blk(coords_int[0])}
             if fused:
                 outs["fused"] = blk.lookup_conv1x1_relu(coords[0], wt, bias)
             torch.cuda.synchronize()
@@ -65,11 +66,15 @@ with torch.no_grad():
             for op in outs:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for c in (coords_int if op == "lookup_int" else coords):
-                    blk(c) if op.startswith("lookup") else blk.lookup_conv1x1_relu(c, wt, bias)
+                if op == "build":
+                    for _ in range(3):
+                        eraft_amd.CorrBlock(f1, f2)
+                else:
+                    for c in (coords_int if op == "lookup_int" else coords):
+                        blk(c) if op.startswith("lookup") else blk.lookup_conv1x1_relu(c, wt, bias)
                 e1.record()
                 torch.cuda.synchronize()
-                times[(name, op)].append(e0.elapsed_time(e1) / len(coords))
+                times[(name, op)].append(e0.elapsed_time(e1) / (3 if op == "build" else len(coords)))
 for (name, op), ts in times.items():
     if not ts:
         continue
