@@ -360,7 +360,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 // PK (split mode, default): the operands arrive pre-split by pack_kernel as 8-KB panels (one per
 // 128-pixel tile and 16-deep K chunk) laid out in MFMA-fragment order, so LDS-DMA copies them
 // verbatim and each fragment is ONE lane-linear ds_read_b128: no VALU work in the K loop, no zero
-// fill (the panels carry their padding).
+// fill (the panels carry their padding).  The MFMAs take the fmap2 fragment as their A operand,
+// so the accumulators hold C^T and reach the LDS C tile as 16-byte stores.
 // ABL (A/B ablation of the pipelined PK loop only, output invalid; ECORR_BUILD_ABL): 5 no MFMA,
 // 6 no fragment reads, 7 no barrier, 8 no chunk copies -- each also without the epilogue.
 template <bool VEC, int KB, bool HALF, bool NTS, int GBUF = 0, bool SPLIT = false, bool PK = false, int ABL = 0>
@@ -485,18 +486,18 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
             const halfx8 b0l = *reinterpret_cast<const halfx8*>(bp + 1024);
             const halfx8 b1h = *reinterpret_cast<const halfx8*>(bp + 2048);
             const halfx8 b1l = *reinterpret_cast<const halfx8*>(bp + 3072);
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0l, b0h, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0l, b1h, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l, b0h, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l, b1h, acc[1][1], 0, 0, 0);
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b0l, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b1l, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b0l, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b1l, acc[1][1], 0, 0, 0);
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b0h, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b1h, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b0h, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b1h, acc[1][1], 0, 0, 0);
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0h, a0l, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1h, a0l, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0h, a1l, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1h, a1l, acc[1][1], 0, 0, 0);
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0l, a0h, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1l, a0h, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0l, a1h, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1l, a1h, acc[1][1], 0, 0, 0);
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0h, a0h, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1h, a0h, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0h, a1h, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1h, a1h, acc[1][1], 0, 0, 0);
             return;
         }
         if constexpr (SPLIT) {
@@ -614,21 +615,21 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                         for (int q = 0; q < 8; ++q) asm volatile("" ::"v"(f[q]));
                         return;
                     }
-                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[1], f[4], acc[0][0], 0, 0, 0);
-                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[1], f[6], acc[0][1], 0, 0, 0);
-                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[3], f[4], acc[1][0], 0, 0, 0);
-                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[3], f[6], acc[1][1], 0, 0, 0);
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[4], f[1], acc[0][0], 0, 0, 0);
+                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[6], f[1], acc[0][1], 0, 0, 0);
+                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[4], f[3], acc[1][0], 0, 0, 0);
+                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[6], f[3], acc[1][1], 0, 0, 0);
                 };
                 auto mfma_rest = [&](const halfx8 (&f)[8]) {
                     if constexpr (ABL == 5) return;
-                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[0], f[5], acc[0][0], 0, 0, 0);
-                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[0], f[7], acc[0][1], 0, 0, 0);
-                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[2], f[5], acc[1][0], 0, 0, 0);
-                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[2], f[7], acc[1][1], 0, 0, 0);
-                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[0], f[4], acc[0][0], 0, 0, 0);
-                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[0], f[6], acc[0][1], 0, 0, 0);
-                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[2], f[4], acc[1][0], 0, 0, 0);
-                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[2], f[6], acc[1][1], 0, 0, 0);
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[5], f[0], acc[0][0], 0, 0, 0);
+                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[7], f[0], acc[0][1], 0, 0, 0);
+                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[5], f[2], acc[1][0], 0, 0, 0);
+                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[7], f[2], acc[1][1], 0, 0, 0);
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[4], f[0], acc[0][0], 0, 0, 0);
+                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[6], f[0], acc[0][1], 0, 0, 0);
+                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[4], f[2], acc[1][0], 0, 0, 0);
+                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[6], f[2], acc[1][1], 0, 0, 0);
                 };
                 // chunk j's buffer is j % NBUF; a chunk is issued into the buffer whose reads the
                 // preceding barrier retired.  Exactly one chunk stays in flight at every wait:
@@ -714,14 +715,31 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
+                    for (int j = 0; j < 2; ++j) {
+                        if constexpr (PK) {
+                            // PK tiles are C^T (targets on the rows, queries on the lanes): each
+                            // lane's 4 consecutive rows are 4 consecutive targets of one query, one
+                            // 16-byte LDS store (row stride 132: conflict-free)
+                            const int m = mb + i * 32 + acol;
+                            const int ea = exs[(HALF ? half * 64 : 0) + m];
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int m = mb + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
-                            const int n = wn * 64 + j * 32 + acol;
-                            const int e = SPLIT ? exs[(HALF ? half * 64 : 0) + m] + exs[BM + n] : 0;
-                            Cs[m * CS + n] = scaled(acc[i][j][r], e);
+                            for (int g4 = 0; g4 < 4; ++g4) {
+                                const int n = wn * 64 + j * 32 + 8 * g4 + 4 * arow;
+                                floatx4 v;
+#pragma unroll
+                                for (int t = 0; t < 4; ++t) v[t] = scaled(acc[i][j][4 * g4 + t], ea + exs[BM + n + t]);
+                                *reinterpret_cast<floatx4*>(Cs + m * CS + n) = v;
+                            }
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) {
+                                const int m = mb + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
+                                const int n = wn * 64 + j * 32 + acol;
+                                const int e = SPLIT ? exs[(HALF ? half * 64 : 0) + m] + exs[BM + n] : 0;
+                                Cs[m * CS + n] = scaled(acc[i][j][r], e);
+                            }
                         }
+                    }
             };
             if (P.scale_is_mul) {
                 // v * 2^-(e1+e2) * 2^-s as one exact scaling (unless subnormal) when 1/sqrt(D) = 2^-s

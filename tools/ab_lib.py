@@ -60,7 +60,11 @@ with torch.no_grad():
             if rnd < 2:
                 for op, o in outs.items():
                     if op in ref:
-                        assert torch.equal(o, ref[op]), f"{name} {op} output differs"
+                        if os.environ.get("AB_ALLOW_DIFF"):   # numerically different variants
+                            d = (o - ref[op]).abs().max().item() if o.shape == ref[op].shape else float("nan")
+                            print(f"{name} {op}: max |diff| vs first {d:.3g}", flush=True)
+                        else:
+                            assert torch.equal(o, ref[op]), f"{name} {op} output differs"
                     else:
                         ref[op] = o.clone()
             for op in outs:
