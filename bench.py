@@ -403,7 +403,7 @@ def main():
     bind, other = (mfma_roof, hbm_roof) if t_mfma >= t_hbm else (hbm_roof, mfma_roof)
     kernels = {
         "build": dict(bind, ms_per_launch=round(build_ms, 4), mode=mode,
-                      covers=("pack_kernel<false> + pack_kernel<true> + build_kernel (one CorrBlock build; "
+                      covers=("pack_both_kernel (both operand passes, one launch) + build_kernel (one CorrBlock build; "
                               "HIP events on the launch stream)") if mode == "split" else "build_kernel",
                       other_roof={k: other[k] for k in ("bound", "achieved", "peak", "unit", "frac")}),
         "lookup": {"bound": "hbm", "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -420,8 +420,15 @@ def main():
     ideal_s = max(t_mfma, t_hbm) + iters * look_bytes / (PEAK_HBM_GBS * 1e9)
     pairs = (world * B if a.mode == "batch" else B) * a.steps
     if a.mode == "batch":
-        cfg = {"workload": f"DSEC 480x640 CorrBlock build + {iters} lookups, warm-start, batch {B} per GPU "
-                           f"(BASELINE configs[1]; N>1 = configs[3])",
+        if (H, W) == (60, 80):
+            wl = f"DSEC 480x640 CorrBlock build + {iters} lookups, warm-start, batch {B} per GPU " \
+                 f"(BASELINE configs[1]; N>1 = configs[3])"
+        elif (H, W) == (32, 32):
+            wl = f"MVSEC 256x256 crop CorrBlock build + {iters} lookups, warm-start, batch {B} per GPU " \
+                 f"(BASELINE configs[2])"
+        else:
+            wl = f"{8 * H}x{8 * W} input CorrBlock build + {iters} lookups, warm-start, batch {B} per GPU"
+        cfg = {"workload": wl,
                "global_batch": world * B, "fmap": [D, H, W], "levels": 4, "radius": 4,
                "parallelism": f"dp{world} batch-sharded, no collective"}
     else:

@@ -813,8 +813,8 @@ __global__ __launch_bounds__(256) void fmap_exp_kernel(const float* __restrict__
 // (or 4 x 32 band) target block in its LDS column order.  Block = 64 positions x 4 chunk
 // quarters; grid (2 * tiles, B).  The second pass re-reads the block's 64 KB (L2 / MALL hits).
 template <bool ISB>
-__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, BuildParams P, int* __restrict__ ex,
-                                                   char* __restrict__ pack) {
+__device__ __forceinline__ void pack_body(const float* __restrict__ x, const BuildParams& P, int* __restrict__ ex,
+                                          char* __restrict__ pack) {
     __shared__ float red[4][64];
     const int b = blockIdx.y, tile = blockIdx.x >> 1, pos = (blockIdx.x & 1) * 64 + (threadIdx.x & 63);
     const int qtr = threadIdx.x >> 6, D = P.D, dc = (D + 15) / 16;
@@ -891,6 +891,27 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, 
             w[kk] = (pix >= 0 && k < D) ? px[(int64_t)k * N] : 0.f;
         }
         put(c, w);
+    }
+}
+
+template <bool ISB>
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, BuildParams P, int* __restrict__ ex,
+                                                   char* __restrict__ pack) {
+    pack_body<ISB>(x, P, ex, pack);
+}
+
+// Both operand passes in ONE launch: grid (2 * max(n_mt, n_nt), B, 2), z = 0 packs fmap1 (slab
+// tiles), z = 1 fmap2 (target blocks).  Neither pass alone fills the chip (1,216 blocks at DSEC
+// B = 16, all resident at once, latency-bound on their 64 loads per thread); one grid overlaps
+// the two and drops a launch boundary: build 0.836 -> 0.826 ms at DSEC B = 16 (rotated A/B,
+// profiles/r01_final8/ab_pack.txt; a 128-VGPR cap for 4 waves per SIMD spills and gains nothing,
+// 0.829).  Surplus x blocks of the shorter pass return at once (block-uniform, before
+// pack_body's barrier).
+__global__ __launch_bounds__(256) void pack_both_kernel(BuildParams P) {
+    if (blockIdx.z == 0) {
+        if ((int)blockIdx.x < 2 * P.n_mt) pack_body<false>(P.f1, P, P.ex1, const_cast<char*>(P.pk1));
+    } else if ((int)blockIdx.x < 2 * P.n_nt) {
+        pack_body<true>(P.f2, P, P.ex2, const_cast<char*>(P.pk2));
     }
 }
 
@@ -988,10 +1009,16 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
         const bool pk = !(kp && atoi(kp) == 0) &&
                         (int64_t)(P.n_mt > P.n_nt ? P.n_mt : P.n_nt) * ((P.D + 15) / 16) * 8192 < 0x7fff0000LL;
         if (pk) {
-            hipLaunchKernelGGL(pack_kernel<false>, dim3((unsigned)(2 * P.n_mt), B), dim3(256), 0, stream, P.f1, P,
-                               P.ex1, P.ws + w.pk1);
-            hipLaunchKernelGGL(pack_kernel<true>, dim3((unsigned)(2 * P.n_nt), B), dim3(256), 0, stream, P.f2, P,
-                               P.ex2, P.ws + w.pk2);
+            const char* k2 = getenv("ECORR_BUILD_PACK2");   // dev knob (A/B): 1 = one launch per operand
+            if (k2 && atoi(k2) == 1) {
+                hipLaunchKernelGGL(pack_kernel<false>, dim3((unsigned)(2 * P.n_mt), B), dim3(256), 0, stream, P.f1, P,
+                                   P.ex1, P.ws + w.pk1);
+                hipLaunchKernelGGL(pack_kernel<true>, dim3((unsigned)(2 * P.n_nt), B), dim3(256), 0, stream, P.f2, P,
+                                   P.ex2, P.ws + w.pk2);
+            } else {
+                const int nx = 2 * (P.n_mt > P.n_nt ? P.n_mt : P.n_nt);
+                hipLaunchKernelGGL(pack_both_kernel, dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
+            }
             const char* ka = getenv("ECORR_BUILD_ABL");   // dev knob: loop ablations (A/B only)
             switch (ka && P.dev_pk_pipe ? atoi(ka) : 0) {
                 case 5: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true, 5>), grid, block, 0, stream, P); break;

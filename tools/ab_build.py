@@ -21,7 +21,7 @@ if os.environ.get("AB_VARIANTS"):
     import json
     VARIANTS = json.loads(os.environ["AB_VARIANTS"])
 KNOBS = ("ECORR_BUILD_SKIP_EPILOGUE", "ECORR_BUILD_KB32", "ECORR_BUILD_NOBAND", "ECORR_BUILD_GLDS",
-         "ECORR_BUILD_PK", "ECORR_BUILD_PKPIPE", "ECORR_BUILD_GM", "ECORR_BUILD_ABL")
+         "ECORR_BUILD_PK", "ECORR_BUILD_PACK2", "ECORR_BUILD_PKPIPE", "ECORR_BUILD_GM", "ECORR_BUILD_ABL")
 B = int(os.environ.get("AB_BATCH", "16"))
 H, W, D = 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)
