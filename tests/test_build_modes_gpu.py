@@ -119,3 +119,22 @@ def test_split_inloop_fallback(ea, case, monkeypatch):
     ref_levels = oracle.pyramid_from_level0(lv[0], 3)
     for i in range(1, 3):
         assert oracle.same_bits(lv[i], ref_levels[i]), f"level {i}"
+
+
+@pytest.mark.parametrize("case", [(2, 256, 16, 24, 1.0, 9), (3, 100, 17, 22, 1e-3, 10), (1, 256, 60, 80, 1.0, 11),
+                                  (2, 64, 5, 300, 3e4, 12)],
+                         ids=lambda c: "b%d_d%d_%dx%d_s%g" % c[:5])
+def test_split_single_pack_launch_matches_two(ea, case, monkeypatch):
+    """Both operand passes run as ONE launch (pack_both_kernel, grid z = operand, surplus x blocks
+    of the shorter pass return at once).  Shapes with n_mt != n_nt (ragged 17x22, the band tiles of
+    a 5-row map, DSEC 60x80) must give the pyramid bit for bit as one launch per operand
+    (ECORR_BUILD_PACK2=1, read per launch)."""
+    B, D, H, W, scale, seed = case
+    f1 = torch.from_numpy((prng.normal(10 * seed, (B, D, H, W)) * np.float32(scale)).astype(np.float32)).to(DEV)
+    f2 = torch.from_numpy((prng.normal(10 * seed + 1, (B, D, H, W)) * np.float32(scale)).astype(np.float32)).to(DEV)
+    with torch.no_grad():
+        one = _build(ea, f1, f2, "split", levels=3)
+        monkeypatch.setenv("ECORR_BUILD_PACK2", "1")
+        two = _build(ea, f1, f2, "split", levels=3)
+    for i in range(3):
+        assert oracle.same_bits(one[i], two[i]), f"level {i}"
