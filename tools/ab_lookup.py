@@ -13,6 +13,9 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import eraft_amd  # noqa: E402
 
 VARIANTS = {"cols3reg": {}, "cols3": {"ECORR_LOOKUP_V": "3"}, "staged4": {"ECORR_LOOKUP_V": "4"}}
+if os.environ.get("AB_VARIANTS"):   # '{"name": {"KNOB": "v", ...}, ...}'
+    import json
+    VARIANTS = json.loads(os.environ["AB_VARIANTS"])
 KNOBS = ("ECORR_LOOKUP_QB", "ECORR_LOOKUP_V", "ECORR_LOOKUP_SKIP")
 B, H, W, D = int(os.environ.get("AB_BATCH", "16")), 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)
