@@ -196,7 +196,7 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
             }
         }
     }
-    if (P.fused_levels >= 3 && tid < 2 * MR) {   // level 2: rows ty0/4 + {0,1}, cols tx0/4 .. +3
+    if (P.fused_levels >= 3 && tid < 2 * MR && P.dev_skip_epilogue != -1 && P.dev_skip_epilogue != -4) {   // level 2: rows ty0/4 + {0,1}, cols tx0/4 .. +3
         const int mm = tid >> 1, y = tid & 1;
         if (mm < mvalid) {
             const float* src = S2 + mm * P2S + y * 4;
@@ -217,7 +217,7 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
             }
         }
     }
-    if (P.fused_levels >= 4 && tid < MR && tid < mvalid) {   // level 3: row ty0/8, cols tx0/8 .. +1
+    if (P.fused_levels >= 4 && tid < MR && tid < mvalid && P.dev_skip_epilogue != -1 && P.dev_skip_epilogue != -3) {   // level 3: row ty0/8, cols tx0/8 .. +1
         const float* src = S3 + tid * 2;
         float* img = P.lvl[3] + (row0 + tid) * P.lsz[3];
         if (P.lntx[3] > 0) {
@@ -314,7 +314,7 @@ __device__ __forceinline__ void epilogue_band(const BuildParams& P, const TileCo
             }
         }
     }
-    if (P.fused_levels >= 3 && tid < 2 * MR) {   // level 2: row ty0/4, cols tx0/4 .. +7
+    if (P.fused_levels >= 3 && tid < 2 * MR && P.dev_skip_epilogue != -1 && P.dev_skip_epilogue != -4) {   // level 2: row ty0/4, cols tx0/4 .. +7
         const int mm = tid >> 1, hf = tid & 1;
         if (mm < mvalid) {
             const float* src = S2 + mm * P2S + hf * 4;
