@@ -42,7 +42,7 @@ struct BuildParams {
     int n_reg, band_y0;  // regular (8 x 16) n-tiles per m-tile; first row of the 4-row band tiles
     int fused_levels;   // levels written by the GEMM epilogue (<= 4)
     int dev_skip_epilogue;  // A/B ablation only (ECORR_BUILD_SKIP_EPILOGUE): 1 no epilogue, 2 no level-0 stores,
-                            // -1 / -4 / -3 no level-2+3 / level-2 / level-3 stores
+                            // -1 / -4 / -3 no level-2+3 / level-2 / level-3 stores, -5 scalar level-3 stores
     float* lvl[4];
     int lh[4], lw[4];
     int lntx[4], lnty[4];   // tiles per tile row (0 = compact row-major) / tile rows of each fused level
