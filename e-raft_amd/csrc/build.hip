@@ -1,27 +1,21 @@
-// build.hip -- CorrBlock build on gfx950: all-pairs correlation GEMM on fp32 MFMA with the
-// 1/sqrt(D) scale and the 3 pooled pyramid levels fused into the epilogue.
+// build.hip -- CorrBlock build on gfx950: the all-pairs correlation GEMM with the 1/sqrt(D) scale
+// and the 3 pooled pyramid levels fused into its epilogue.
 //
 // Replaces corr.py:13-27 (CorrBlock.__init__) and corr.py:52-60 (CorrBlock.corr):
 //   level0[b*q_count + p][y][x] = (sum_d f1[b][d][p] * f2[b][d][y*W+x]) / sqrt(D)
 //   level{i+1} = (((x00 + x01) + x10) + x11) / 4 over 2x2 floor-mode windows of level i,
 // stored in the tiled pyramid layout of include/ecorr.h (4 x 8-float tiles per query image).
 //
-// GEMM view per batch item: A = f1[b] as [K=D][M=q_count] (queries contiguous), B = f2[b] as
-// [K][N=H*W].  Block tile: 128 queries x one 8x16 block of target pixels (N = 128), K staged 32
-// deep through double-buffered LDS by float4 register staging; 4 waves, each 64x64 = 2x2
-// v_mfma_f32_32x32x2_f32 tiles.  The N tile is a 2-D target block (2 x 2 pyramid tiles of level
-// 0, exactly one tile of level 1), so the epilogue pools locally and every level-0/1 store is a
-// whole 128-byte tile.
+// Two GEMMs, one result contract (include/ecorr.h):
+//   split (ecorr_build_split, default): pack_both_kernel splits every fp32 operand into
+//     per-pixel-scaled f16 hi + lo halves, written as 8-KB panels in MFMA-fragment order;
+//     build_split_kernel sums lo*hi + hi*lo + hi*hi per product on v_mfma_f32_32x32x16_f16.
+//   fp32 (ecorr_build): build_kernel on v_mfma_f32_32x32x2_f32, an exact k-ordered fmaf chain.
+// Pooling is bit-exact given the same level 0 in both; per-element accumulation order does not
+// depend on the tiling, so query-slab (row-sharded) builds are bitwise the whole build's rows.
 //
-// Numerics: MFMA f32 is an exact k-ordered fmaf chain; the per-element k order does not depend on
-// the tiling, so sharded and unsharded builds agree bit for bit.  Against the reference's sgemm
-// level 0 agrees normwise (max|d|/rms <= 1e-5); pooling is bit-exact given the same level 0.
-//
-// A/B history (tools/ab_build.py): a k-permuted LDS layout with one ds_read_b128
-// per 4 MFMA steps, persistent tiles, and two K chunks of loads in flight were all slower on
-// MI355X; per-thread scattered epilogue stores cost 14%.
-#include <stdlib.h>
-
+// There are no runtime knobs: every variant that lost an A/B is gone from the source (DESIGN.md
+// §3.1 keeps the record); lab builds for new A/Bs are separate .so files (tools/).
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
 
@@ -29,35 +23,472 @@ namespace ecorr {
 
 namespace {
 
-constexpr int BM = 128;           // queries per block tile
-constexpr int TBH = 8, TBW = 16;  // target block (rows x cols) per block tile
-constexpr int BN = TBH * TBW;     // 128 targets
-constexpr int NT = 256;           // threads
-constexpr int CS = BN + 4;        // C-tile LDS row stride (floats): conflict-free ds_read_b128
-constexpr int P1S = 36, P2S = 12;  // LDS per-query strides of the pooled staging (conflict-free)
-
-// LDS floats for K chunk KB (double-buffered A and B, row strides AS / BS) and a C tile of MR
-// query rows.
-constexpr int smem_floats(int KB, int MR, int AS, int BS, int NBUF = 2) {
-    return NBUF * (KB * AS + KB * BS) > MR * CS ? NBUF * (KB * AS + KB * BS) : MR * CS;
-}
-
-// 16-byte pyramid store; NTS = non-temporal: the 2 GB pyramid is not re-read by this kernel, and
-// streaming it past the caches took 5% off the build (tools/ab_build.py)
-template <bool NTS, typename V>
-__device__ __forceinline__ void st(V* p, V v) {
-    if (NTS) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef unsigned uint4v __attribute__((ext_vector_type(4)));
+typedef unsigned uint2v __attribute__((ext_vector_type(2)));
 
-// Split mode: x * 2^e = hi + lo + O(2^-22 |x|), hi = f16(x 2^e), lo = f16(x 2^e - hi) (the
-// subtraction is exact).  e puts the pixel's largest |value| in [2^14, 2^15), so hi never
-// overflows and lo stays normal for all but values 2^17 below that maximum.
+constexpr int TBH = 8, TBW = 16;  // regular target block (rows x cols) of one n-tile
+constexpr int PANEL = 8192;       // bytes of one (128-pixel tile, 16-deep K chunk) operand panel
+
+__device__ __forceinline__ float pool4(float a, float b, float c, float d) {
+    return __fmul_rn(__fadd_rn(__fadd_rn(__fadd_rn(a, b), c), d), 0.25f);
+}
+
+// 2^e as a float, e in [-126, 127]
+__device__ __forceinline__ float exp2i(int e) { return __int_as_float((e + 127) << 23); }
+
+// s_waitcnt vmcnt(N) with lgkmcnt(0) (LGKM0) or left alone; expcnt never waited (N < 16)
+template <int N, bool LGKM0>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 16, "vmcnt field");
+    __builtin_amdgcn_s_waitcnt(N | (7 << 4) | (LGKM0 ? 0 : (15 << 8)));
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 T1): consecutive logical tiles land on
+// one XCD so tiles sharing operand panels share that XCD's L2.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, k = bid / 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+// n-tiles: 8 x 16 target blocks (regular), or, in the last 4 rows when H % 8 is 1..4, 4 x 32
+// blocks ("band"): those rows feed pyramid levels 0-2 only (level 3 of an H = 8k + r map, r <= 4,
+// has k rows), so the band pools 4 x 8 sub-blocks and no 8-row tile row is padded half empty
+// (DSEC H = 60: 6.7% of the matrix work saved).
+struct NTile { int ty0, tx0, band; };
+__device__ __forceinline__ NTile ntile_of(const BuildParams& P, int nt) {
+    NTile n;
+    if (nt < P.n_reg) {
+        const int nty = nt / P.n_ntx;
+        n.ty0 = nty * TBH;
+        n.tx0 = (nt - nty * P.n_ntx) * TBW;
+        n.band = 0;
+    } else {
+        n.ty0 = P.band_y0;
+        n.tx0 = (nt - P.n_reg) * 32;
+        n.band = 1;
+    }
+    return n;
+}
+
+// Grouped tile order: GM m-tiles x all n-tiles per group, so consecutive tiles share panels.
+__device__ __forceinline__ void decode_tile(const BuildParams& P, int t, int n_m, int& b, int& mt, int& nt) {
+    constexpr int GM = 8;
+    const int per_b = n_m * P.n_nt;
+    b = t / per_b;
+    const int i = t - b * per_b;
+    const int gsz = GM * P.n_nt;
+    const int grp = i / gsz, gi = i - grp * gsz;
+    const int first_m = grp * GM;
+    const int gsm = min(n_m - first_m, GM);
+    mt = first_m + gi % gsm;
+    nt = gi / gsm;
+}
+
+// One pooled-level pixel (row, col) of a query image: tiled (ntx > 0; the tile must exist, cells
+// in a tile's padding are written and never read) or compact row-major (range-checked).
+__device__ __forceinline__ float* level_px(const BuildParams& P, int L, int64_t row_img, int r, int c) {
+    float* img = P.lvl[L] + row_img * P.lsz[L];
+    if (P.lntx[L] > 0) {
+        if ((r >> 2) >= P.lnty[L] || (c >> 3) >= P.lntx[L]) return nullptr;
+        return img + tiled_off(r, c, P.lntx[L]);
+    }
+    if (r >= P.lh[L] || c >= P.lw[L]) return nullptr;
+    return img + (int64_t)r * P.lw[L] + c;
+}
+
+// ============================================================================================
+// Split GEMM (default).  Block tile: 256 queries (two 128-query fmap1 panels) x one 128-target
+// n-tile (one fmap2 panel); 4 waves, wave w = queries 64 w .. 64 w + 63 x all 128 targets = 2 x 4
+// v_mfma_f32_32x32x16_f16 tiles (128 accumulators, pinned to AGPRs), so every K chunk reads 12
+// fragments for 24 MFMAs (0.5 KB of LDS per MFMA, 0.67 in round 1).  Two blocks per CU.
+//
+// The MFMAs take the fmap2 fragment as their A operand: the accumulators hold C^T, lane (acol,
+// arow) of tile (i, j) owns query 32 i + acol and targets 32 j + 8 g4 + 4 arow + t (reg 4 g4 + t).
+// The fmap2 panel stores the n-tile's targets (split_target) so that target group j of a regular
+// 8 x 16 tile is one pyramid tile line: rows 4 (j & 1) + g4, cols 8 (j >> 1) + 4 arow + t -- each
+// lane holds 4 x 4 pixels of every line of its query, the 2 x 2 and 4 x 4 pools are in-lane and
+// the 8 x 8 pool needs one value from lane acol + 32.  Band tiles (4 x 32): rows g4, cols 8 j +
+// 4 arow + t.
+//
+// K loop: each 16-deep chunk's three panels (24 KB) go global -> LDS verbatim by LDS-DMA
+// (buffer_load_dwordx4 ... lds, 6 per wave) through 3 buffers, one chunk in flight behind the one
+// being read; one barrier per chunk; fragments are lane-linear ds_read_b128 (conflict-free).
+// Chunk kc + 1's barrier and first fragments are read between chunk kc's lo*hi MFMAs and its
+// hi*lo / hi*hi MFMAs.  Chunks past the end are issued as out-of-range loads (they land as
+// zeros), which keeps every wait count static.
+//
+// Epilogue, straight from the accumulators (no LDS, no barrier): scale by 2^-(e_q + e_t) /
+// sqrt(D), pool 8x8 -> 4x4 -> 2x2 -> 1 in registers in the reference's order, then store.  Store
+// shape matters more than anything else here (tools/store_lab.hip, DSEC level-0 shape): 32-byte
+// pieces per query per instruction run at 5.2 TB/s only as plain stores, which keep every line
+// in L2 and evict the operand panels (PMC: 1 GB of panel re-reads per build instead of 0.33 GB);
+// 64-byte pieces run at 5.3-5.5 TB/s with sc1 stores, which leave L2 right away.  So levels 0
+// and 1 are assembled into 64-byte line segments in registers -- v_permlane32_swap gives lane
+// acol rows 0-1 and lane acol + 32 rows 2-3 of a line, a DPP transpose over each 4-lane quad
+// gives 4 adjacent lanes the 4 pieces of one query's segment -- and every store instruction
+// writes 8 whole 128-byte lines.  Levels 2-3 (6% of the bytes) are single pixels, plain stores.
+// ============================================================================================
+constexpr int SQ = 256;                     // queries per split tile
+constexpr int SCHUNK = 3 * PANEL;           // LDS bytes per K chunk (2 query panels + 1 target panel)
+constexpr int SNBUF = 3;
+constexpr int SCOPIES = SCHUNK / 1024 / 4;  // LDS-DMA copies per wave per chunk (6)
+constexpr int SOOB = 0x7ffffff0;            // buffer offset beyond any panel: loads 0, touches nothing
+constexpr int ST_SC1 = 18;                  // level-0/1 store cache policy: nt sc1 (write through, drop from L2)
+constexpr int XS = 144;                     // LDS bytes per query of the epilogue's line transpose
+
+// target (y, x) of position p of a split fmap2 panel, relative to the n-tile origin
+__host__ __device__ __forceinline__ void split_target(int p, bool band, int& y, int& x) {
+    if (!band) {
+        y = 4 * ((p >> 5) & 1) + ((p >> 3) & 3);
+        x = 8 * (p >> 6) + (p & 7);
+    } else {
+        y = (p >> 3) & 3;
+        x = 8 * (p >> 5) + (p & 7);
+    }
+}
+
+// lanes 32-63 of a <-> lanes 0-31 of b (v_permlane32_swap)
+__device__ __forceinline__ void swap32(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+
+template <bool MUL>
+__global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
+    // ALL LDS in this one array: a second __shared__ object can make hipcc wait vmcnt(0) before
+    // every ds_read while a buffer_load ... lds is in flight (cdna_hip_programming.md trap 4(a))
+    __shared__ __attribute__((aligned(16))) char smem[SNBUF * SCHUNK + (SQ + 128) * 4];
+    int* exq = reinterpret_cast<int*>(smem + SNBUF * SCHUNK);   // exponents of the 256 queries
+    int* ext = exq + SQ;                                        // ... and of the 128 panel targets
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int acol = lane & 31, arow = lane >> 5;
+    int b, qt, nt;
+    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    const NTile tc = ntile_of(P, nt);
+    const int q0 = qt * SQ;
+    const int H = P.H, W = P.W;
+    const int64_t Q = (int64_t)H * W;
+
+    {   // per-pixel exponents (written before the first barrier; the K loop's first wait drains
+        // them with lgkmcnt(0))
+        exq[tid] = q0 + tid < P.q_count ? P.ex1[(int64_t)b * P.q_count + q0 + tid] : 0;
+        if (tid < 128) {
+            int y, x;
+            split_target(tid, tc.band, y, x);
+            y += tc.ty0;
+            x += tc.tx0;
+            ext[tid] = (y < H && x < W) ? P.ex2[(int64_t)b * Q + (int64_t)y * W + x] : 0;
+        }
+    }
+
+    // ---- operand panels of this tile: two query panels (adjacent tiles of pk1), one target panel
+    const int dc = (P.D + 15) / 16, nk = dc;
+    const int64_t pstride = (int64_t)dc * PANEL;   // bytes of one 128-pixel tile's panels
+    const int qp = 2 * qt;
+    const int nqp = min(2, P.n_mt - qp);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(P.pk1 + ((int64_t)b * P.n_mt + qp) * pstride), 0, (int)(nqp * pstride), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(P.pk2 + ((int64_t)b * P.n_nt + nt) * pstride), 0, (int)pstride, 0x00020000);
+    // copy s of this wave: 1-KB piece c = wave + 4 s of the chunk (pieces 0-15: query panels, 16-23:
+    // the target panel); lane-linear, as LDS-DMA requires
+    auto issue = [&](int kc) {
+        char* dst = smem + (kc % SNBUF) * SCHUNK;
+        const bool in = kc < nk;
+#pragma unroll
+        for (int s = 0; s < SCOPIES; ++s) {
+            const int c = wave + 4 * s;
+            if (s < 4) {
+                const int off = (c >> 3) * (int)pstride + kc * PANEL + (c & 7) * 1024 + lane * 16;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rq, (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, in ? off : SOOB, 0, 0, 0);
+            } else {
+                const int off = kc * PANEL + (c - 16) * 1024 + lane * 16;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rt, (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, in ? off : SOOB, 0, 0, 0);
+            }
+        }
+    };
+
+    floatx16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    // pin the accumulators to AGPRs: left to its heuristics hipcc keeps them in VGPRs with MFMA
+    // destinations apart from their sources and spills ~100 registers at 2 waves per SIMD
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
+
+    // fragments of one chunk: query i hi/lo (query panel wave/2, 32-row group 2 (wave&1) + i),
+    // target j hi/lo (target panel, group j); panel group = [hi k0-15 | lo k0-15] x 32 rows, 16 B
+    // per lane
+    const int qfo = (wave >> 1) * PANEL + (wave & 1) * 4096 + lane * 16;
+    const int tfo = 2 * PANEL + lane * 16;
+    struct Frags { halfx8 qh[2], ql[2], th[4], tl[4]; };
+    auto read_lo = [&](int kc, Frags& f) {   // what the lo*hi MFMAs need: ql, th
+        const char* cb = smem + (kc % SNBUF) * SCHUNK;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) f.ql[i] = *reinterpret_cast<const halfx8*>(cb + qfo + i * 2048 + 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f.th[j] = *reinterpret_cast<const halfx8*>(cb + tfo + j * 2048);
+    };
+    auto read_hi = [&](int kc, Frags& f) {   // qh, tl
+        const char* cb = smem + (kc % SNBUF) * SCHUNK;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) f.qh[i] = *reinterpret_cast<const halfx8*>(cb + qfo + i * 2048);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f.tl[j] = *reinterpret_cast<const halfx8*>(cb + tfo + j * 2048 + 1024);
+    };
+    // per element: lo*hi, then hi*lo, then hi*hi (the accumulation order of the round-1 build)
+    auto mfma_lohi = [&](const Frags& f) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.th[j], f.ql[i], acc[i][j], 0, 0, 0);
+    };
+    auto mfma_rest = [&](const Frags& f) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.tl[j], f.qh[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.th[j], f.qh[i], acc[i][j], 0, 0, 0);
+    };
+    // chunk j's copies landed (the chunk after it may fly), this wave's earlier fragment reads
+    // are done; the barrier publishes chunk j and retires every wave's reads of chunk j - 1, whose
+    // buffer chunk j + 2 then takes
+    auto advance = [&](int j) {
+        wait_vm<SCOPIES, true>();
+        __builtin_amdgcn_s_barrier();
+        issue(j + 2);
+    };
+
+    Frags fa, fb;
+    issue(0);
+    issue(1);
+    advance(0);
+    read_lo(0, fa);
+    read_hi(0, fa);
+    for (int kc = 0; kc < nk; kc += 2) {
+        mfma_lohi(fa);
+        advance(kc + 1);
+        read_lo(kc + 1, fb);
+        mfma_rest(fa);
+        read_hi(kc + 1, fb);
+        if (kc + 1 >= nk) break;   // odd chunk count: fb is a zero chunk
+        mfma_lohi(fb);
+        advance(kc + 2);
+        read_lo(kc + 2, fa);
+        mfma_rest(fb);
+        read_hi(kc + 2, fa);
+    }
+    wait_vm<0, true>();             // the trailing zero chunks have landed and this wave's reads are done ...
+    __builtin_amdgcn_s_barrier();   // ... in every wave: the chunk buffers are the epilogue's scratch
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
+
+    // ---------------- epilogue (per wave, from registers) ----------------
+    // Line segments through a wave-private LDS transpose (no barrier: a wave's LDS accesses are
+    // processed in order): the lane writes its 16-byte pieces into the line image of its query
+    // (32 queries x 144 B: conflict-free ds_write_b128 and ds_read_b128), then reads back piece m
+    // of segment arow of query 4k + s, so the 4 lanes of a quad store 64 contiguous bytes and
+    // lanes acol, acol + 32 the two halves of one line.
+    char* xp = smem + wave * (32 * XS);
+    const int m4 = lane & 3, k4 = acol >> 2;
+    const int wo = acol * XS, ro = (4 * k4) * XS + 64 * arow + 16 * m4;
+    const int L = P.fused_levels;
+    const int64_t rows0 = (int64_t)b * P.q_count + q0;   // the block's first query image
+    const int nq = min(SQ, P.q_count - q0);
+    // per-level descriptors over the block's query images (range check = query bound)
+    auto rsrc_of = [&](int lv) {
+        return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + rows0 * P.lsz[lv], 0, (int)(nq * P.lsz[lv] * 4), 0x00020000);
+    };
+    // read the transposed segments back and store them: line byte offset lo (+ the query image)
+    auto store_lines = [&](__amdgpu_buffer_rsrc_t rs, int64_t lsz, int ql, int lo, bool ok) {
+        floatx4 pc[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) pc[s] = *reinterpret_cast<const floatx4*>(xp + ro + s * XS);
+        const int base = (int)((ql + 4 * k4) * lsz * 4) + lo + 16 * m4;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, pc[s]), rs,
+                                                   ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_SC1);
+    };
+    // N adjacent pixels (r, c .. c + N - 1) of level 2 or 3 (tiled: inside one tile row; compact:
+    // row-major), plain stores; pixels outside the level are dropped
+    auto store_px = [&](__amdgpu_buffer_rsrc_t rs, int lv, int qloc, int r, int c, auto val) {
+        constexpr int N = sizeof(val) / 4;
+        const bool tiled = P.lntx[lv] > 0;
+        const int off = (int)((qloc * P.lsz[lv] + level_off(r, c, P.lntx[lv], P.lw[lv])) * 4);
+        if (tiled || c + N <= P.lw[lv]) {   // whole vector in (tiled: padding cells absorb the rest)
+            const bool in = tiled ? ((r >> 2) < P.lnty[lv] && (c >> 3) < P.lntx[lv]) : r < P.lh[lv];
+            if constexpr (N == 4)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, 0);
+            else
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, val), rs, in ? off : SOOB, 0, 0);
+        } else {   // compact level, ragged right edge
+#pragma unroll
+            for (int k = 0; k < N; ++k)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val[k]), rs,
+                                                      r < P.lh[lv] && c + k < P.lw[lv] ? off + 4 * k : SOOB, 0, 0);
+        }
+    };
+    const __amdgpu_buffer_rsrc_t r0 = rsrc_of(0);
+    const __amdgpu_buffer_rsrc_t r1 = rsrc_of(L > 1 ? 1 : 0);
+    const __amdgpu_buffer_rsrc_t r2 = rsrc_of(L > 2 ? 2 : 0);
+    const __amdgpu_buffer_rsrc_t r3 = rsrc_of(L > 3 ? 3 : 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ql = wave * 64 + 32 * i;          // first block-local query of this tile row
+        const int nqe = -(exq[ql + acol] + (MUL ? P.scale_shift : 0));
+        // level-1 values of the lane's query: [block bb][row][col pair] (band: [half][2 y1 + jl]);
+        // level 2: [bb][row r] (band: [bb][jl]); level 3: [bb]
+        float l1[2][4][2], l2[2][2], l3[2];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            __builtin_amdgcn_sched_barrier(0);
+            // scaled values of lines j = 2 bb + jl, [jl][g4][t]; target exponents
+            // ext[32 j + 8 g4 + 4 arow + t]
+            float v[2][4][4];
+#pragma unroll
+            for (int jl = 0; jl < 2; ++jl) {
+                const int j = 2 * bb + jl;
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const int4 e4 = *reinterpret_cast<const int4*>(ext + 32 * j + 8 * g4 + 4 * arow);
+                    const int e[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const float x = ldexpf(acc[i][j][4 * g4 + t], nqe - e[t]);
+                        v[jl][g4][t] = MUL ? x : __fdiv_rn(x, P.scale);
+                    }
+                }
+            }
+            // level 0: line j = rows g4 x this lane's 4 columns
+#pragma unroll
+            for (int jl = 0; jl < 2; ++jl) {
+                __builtin_amdgcn_sched_barrier(0);
+                const int j = 2 * bb + jl;
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4)
+                    *reinterpret_cast<floatx4*>(xp + wo + 32 * g4 + 16 * arow) =
+                        floatx4{v[jl][g4][0], v[jl][g4][1], v[jl][g4][2], v[jl][g4][3]};
+                const int tr = (tc.ty0 >> 2) + (tc.band ? 0 : (j & 1));
+                const int tcl = (tc.tx0 >> 3) + (tc.band ? j : (j >> 1));
+                store_lines(r0, P.lsz[0], ql, ((tr * P.lntx[0] + tcl) * kTile) * 4 + 64 * arow,
+                            tr < P.lnty[0] && tcl < P.lntx[0]);
+            }
+            if (L < 2) continue;
+            if (!tc.band) {
+                // regular: line j = rows 4 jl + g4 of 8 x 8 block bb; level 1 rows y1 = 0..3, cols
+                // 4 bb + 2 arow + c; level 2 rows r, col 2 bb + arow; level 3 needs lane acol + 32
+#pragma unroll
+                for (int y1 = 0; y1 < 4; ++y1)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int jl = y1 >> 1, g = 2 * (y1 & 1);
+                        l1[bb][y1][c] = pool4(v[jl][g][2 * c], v[jl][g][2 * c + 1], v[jl][g + 1][2 * c],
+                                              v[jl][g + 1][2 * c + 1]);
+                    }
+                if (L >= 3) {   // level 2: rows r, col 2 bb + arow (stored per i below)
+#pragma unroll
+                    for (int r = 0; r < 2; ++r)
+                        l2[bb][r] = pool4(l1[bb][2 * r][0], l1[bb][2 * r][1], l1[bb][2 * r + 1][0], l1[bb][2 * r + 1][1]);
+                    // level 3, the 8 x 8 pool: lane acol + 32 holds the right column
+                    const float o0 = __shfl_xor(l2[bb][0], 32), o1 = __shfl_xor(l2[bb][1], 32);
+                    l3[bb] = pool4(l2[bb][0], o0, l2[bb][1], o1);
+                }
+            } else {
+                // band: line j = row g4 x cols 8 j + 4 arow + t; level 1 rows y1 = 0..1, cols
+                // 4 j + 2 arow + c (l1[bb][2 y1 + jl][c]); level 2 col 2 j + arow
+#pragma unroll
+                for (int jl = 0; jl < 2; ++jl)
+#pragma unroll
+                    for (int y1 = 0; y1 < 2; ++y1)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c)
+                            l1[bb][2 * y1 + jl][c] = pool4(v[jl][2 * y1][2 * c], v[jl][2 * y1][2 * c + 1],
+                                                           v[jl][2 * y1 + 1][2 * c], v[jl][2 * y1 + 1][2 * c + 1]);
+                if (L >= 3) {   // level 2: col 2 (2 bb + jl) + arow (stored per i below)
+#pragma unroll
+                    for (int jl = 0; jl < 2; ++jl)
+                        l2[bb][jl] = pool4(l1[bb][jl][0], l1[bb][jl][1], l1[bb][2 + jl][0], l1[bb][2 + jl][1]);
+                }
+            }
+        }
+        if (L < 2) continue;
+        if (L >= 3) {
+            // level 2: one 16-byte row piece per lane.  Regular: the n-tile's 2 x 4 pixels, lane
+            // acol row 0, lane acol + 32 row 1, cols {2 bb, 2 bb + 1} = (l2[bb][0] | l2[bb][1]) after
+            // swapping row 1 of the arow-0 lanes with row 0 of the arow-1 lanes.  Band: the 1 x 8
+            // pixels, lane acol cols 0-3, lane acol + 32 cols 4-7 (swap bb = 1 of the arow-0 lanes
+            // with bb = 0 of the arow-1 lanes)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (!tc.band) swap32(l2[k][0], l2[k][1]);
+                else swap32(l2[0][k], l2[1][k]);
+            }
+            const floatx4 row2 = tc.band ? floatx4{l2[0][0], l2[1][0], l2[0][1], l2[1][1]}
+                                         : floatx4{l2[0][0], l2[0][1], l2[1][0], l2[1][1]};
+            store_px(r2, 2, ql + acol, (tc.ty0 >> 2) + (tc.band ? 0 : arow), (tc.tx0 >> 2) + (tc.band ? 4 * arow : 0), row2);
+            if (L >= 4 && !tc.band)   // level 3: the n-tile's 1 x 2 pixels, from the arow-0 lanes
+                store_px(r3, 3, arow ? nq : ql + acol, tc.ty0 >> 3, tc.tx0 >> 3, floatx2{l3[0], l3[1]});
+        }
+        // level 1 (regular: the n-tile's 4 x 8 level-1 pixels = one tile line; band: rows 0-1 of
+        // two tile lines u = 0, 1, whose segment 0 the lanes acol / acol + 32 store)
+        if (!tc.band) {
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+                for (int y1 = 0; y1 < 4; ++y1)
+                    *reinterpret_cast<floatx2*>(xp + wo + 32 * y1 + 4 * (4 * bb + 2 * arow)) = floatx2{l1[bb][y1][0], l1[bb][y1][1]};
+        } else {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int y1 = 0; y1 < 2; ++y1)
+#pragma unroll
+                    for (int jl = 0; jl < 2; ++jl)
+                        *reinterpret_cast<floatx2*>(xp + wo + 64 * u + 32 * y1 + 4 * (4 * jl + 2 * arow)) =
+                            floatx2{l1[u][2 * y1 + jl][0], l1[u][2 * y1 + jl][1]};
+        }
+        const int r1t = tc.ty0 >> 3;                                   // level-1 tile row
+        const int c1t = (tc.tx0 >> 4) + (tc.band ? arow : 0);          // level-1 tile col
+        store_lines(r1, P.lsz[1], ql, ((r1t * P.lntx[1] + c1t) * kTile) * 4 + (tc.band ? 0 : 64 * arow),
+                    r1t < P.lnty[1] && c1t < P.lntx[1]);
+    }
+}
+
+// Split-mode operand pass: per pixel, ex = 15 - E with max_d |x| = f 2^E, f in [0.5, 1) (so the
+// pixel's largest scaled value lies in [2^14, 2^15); 0 for all-zero or non-finite maxima, so NaN
+// inputs propagate through the GEMM as in the reference), and the f16 split of all D values:
+// x 2^ex = hi + lo + O(2^-22 |x|), hi = f16(x 2^ex), lo = f16(x 2^ex - hi) (the subtraction is
+// exact; lo is exact for values down to 2^-10 of the pixel maximum and keeps 11 bits down to
+// 2^-17 of it -- f16 subnormals below; tests/test_build_modes_gpu.py pins the error over those
+// ranges).  Written as the build's 8-KB panels: panel (tile, chunk) = [32-row group g][hi k0-7 |
+// hi k8-15 | lo k0-7 | lo k8-15][row r][8 halves], i.e. the v_mfma_f32_32x32x16_f16 operand of lane
+// (r, h) is the 16 bytes at g*2048 + part*1024 + lane*16.  Positions without a pixel (ragged
+// edges) and k >= D are zeros.  ISB = 0: fmap1 slab, tile = 128 consecutive queries; ISB = 1:
+// fmap2, tile = the n-tile's targets in split_target order.  Block = 64 positions x 4 chunk
+// quarters; the D <= 256 values of a thread stay in registers between the max and the split.
 __device__ __forceinline__ void split_f16(const float (&v)[8], float s, halfx8& hi, halfx8& lo) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -68,63 +499,127 @@ __device__ __forceinline__ void split_f16(const float (&v)[8], float s, halfx8& 
     }
 }
 
-// 2^e as a float, e in [-126, 127]
-__device__ __forceinline__ float exp2i(int e) { return __int_as_float((e + 127) << 23); }
-
-__device__ __forceinline__ float pool4(float a, float b, float c, float d) {
-    return __fmul_rn(__fadd_rn(__fadd_rn(__fadd_rn(a, b), c), d), 0.25f);
-}
-
-// A tile covers 128 queries x 128 targets: a TBH x TBW = 8 x 16 target block (regular), or, in the
-// last 4 rows when H % 8 is 1..4, a 4 x 32 block ("band"): those rows feed pyramid levels 0-2 only
-// (level 3 of an H = 8k + r map, r <= 4, has k rows), so the band pools 4 x 8 sub-blocks and no
-// 8-row tile row is padded half empty (DSEC H = 60: 6.7% of the MFMA work saved).
-struct TileCoord { int b, m0, ty0, tx0, band, mt, nt; };
-
-// Grouped tile order (8 m-tiles x all n-tiles per group): consecutive tiles share fmap panels.
-__device__ __forceinline__ TileCoord decode_tile(const BuildParams& P, int t) {
-    const int GM = P.gm;
-    const int per_b = P.n_mt * P.n_nt;
-    TileCoord c;
-    c.b = t / per_b;
-    const int i = t - c.b * per_b;
-    const int gsz = GM * P.n_nt;
-    const int grp = i / gsz, gi = i - grp * gsz;
-    const int first_m = grp * GM;
-    const int gsm = min(P.n_mt - first_m, GM);
-    const int mt = first_m + gi % gsm, nt = gi / gsm;
-    c.m0 = mt * BM;
-    c.mt = mt;
-    c.nt = nt;
-    if (nt < P.n_reg) {
-        const int nty = nt / P.n_ntx, ntx = nt - nty * P.n_ntx;
-        c.ty0 = nty * TBH;
-        c.tx0 = ntx * TBW;
-        c.band = 0;
+template <bool ISB>
+__device__ __forceinline__ void pack_body(const float* __restrict__ x, const BuildParams& P, int* __restrict__ ex,
+                                          char* __restrict__ pack) {
+    __shared__ float red[4][64];
+    const int b = blockIdx.y, tile = blockIdx.x >> 1;
+    int pos = (blockIdx.x & 1) * 64 + (threadIdx.x & 63);   // panel position of this lane's pixel
+    const int qtr = threadIdx.x >> 6, D = P.D, dc = (D + 15) / 16;
+    const int64_t N = ISB ? (int64_t)P.H * P.W : (int64_t)P.q_count;
+    int64_t pix = -1;
+    if (!ISB) {
+        const int64_t p = (int64_t)tile * 128 + pos;
+        if (p < P.q_count) pix = p;
     } else {
-        c.ty0 = P.band_y0;
-        c.tx0 = (nt - P.n_reg) * 32;
-        c.band = 1;
+        // lanes in raster order over half the n-tile (16 consecutive pixels per row: 64-byte
+        // reads), each at its panel position (split_target inverted)
+        const NTile n = ntile_of(P, tile);
+        const int h = blockIdx.x & 1, l = threadIdx.x & 63;
+        const int y = n.band ? l >> 4 : 4 * h + (l >> 4), x = n.band ? 16 * h + (l & 15) : l & 15;
+        pos = n.band ? 32 * (x >> 3) + 8 * y + (x & 7) : 64 * (x >> 3) + 32 * (y >> 2) + 8 * (y & 3) + (x & 7);
+        if (n.ty0 + y < P.H && n.tx0 + x < P.W) pix = (int64_t)(n.ty0 + y) * P.W + n.tx0 + x;
     }
-    return c;
+    const float* px = x + (int64_t)b * D * N + (pix < 0 ? 0 : pix);
+    constexpr int CPT = 4;
+    const bool regs = dc <= 4 * CPT;
+    float v[CPT][16];
+    float m = 0.f;
+    if (regs) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) {
+                const int k = (qtr + 4 * i) * 16 + kk;
+                v[i][kk] = (pix >= 0 && k < D) ? px[(int64_t)k * N] : 0.f;
+                m = fmaxf(m, fabsf(v[i][kk]));
+            }
+    } else if (pix >= 0) {
+        for (int k = qtr * 16; k < D; k += 64)
+#pragma unroll 4
+            for (int kk = 0; kk < 16 && k + kk < D; ++kk) m = fmaxf(m, fabsf(px[(int64_t)(k + kk) * N]));
+    }
+    red[qtr][threadIdx.x & 63] = m;
+    __syncthreads();
+    const int l = threadIdx.x & 63;
+    m = fmaxf(fmaxf(red[0][l], red[1][l]), fmaxf(red[2][l], red[3][l]));
+    int E = 0;
+    frexpf(m, &E);
+    int e = (m > 0.f && m <= 3.4028235e38f) ? 15 - E : 0;
+    e = e < -126 ? -126 : (e > 126 ? 126 : e);
+    if (qtr == 0 && pix >= 0) ex[(int64_t)b * N + pix] = e;
+    const float s = exp2i(e);
+    const int ntiles = ISB ? P.n_nt : P.n_mt;
+    char* pan = pack + ((int64_t)b * ntiles + tile) * dc * PANEL + (pos >> 5) * 2048 + (pos & 31) * 16;
+    auto put = [&](int c, const float (&w)[16]) {
+        halfx8 h0, l0, h1, l1;
+        split_f16(*reinterpret_cast<const float(*)[8]>(w), s, h0, l0);
+        split_f16(*reinterpret_cast<const float(*)[8]>(w + 8), s, h1, l1);
+        char* p = pan + (int64_t)c * PANEL;
+        *reinterpret_cast<halfx8*>(p) = h0;
+        *reinterpret_cast<halfx8*>(p + 512) = h1;
+        *reinterpret_cast<halfx8*>(p + 1024) = l0;
+        *reinterpret_cast<halfx8*>(p + 1536) = l1;
+    };
+    if (regs) {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i)
+            if (qtr + 4 * i < dc) put(qtr + 4 * i, v[i]);
+        return;
+    }
+    for (int c = qtr; c < dc; c += 4) {
+        float w[16];
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+            const int k = c * 16 + kk;
+            w[kk] = (pix >= 0 && k < D) ? px[(int64_t)k * N] : 0.f;
+        }
+        put(c, w);
+    }
 }
 
-// Bijective XCD-aware remap (cdna_hip_programming.md §5 T1): consecutive logical tiles land on
-// one XCD so tiles sharing fmap1/fmap2 panels share that XCD's L2.  Speed only, never correctness.
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, k = bid / 8;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+// Both operand passes in ONE launch: grid (2 * max(n_mt, n_nt), B, 2), z = 0 packs fmap1 (128-query
+// tiles), z = 1 fmap2 (n-tiles).  Neither pass alone fills the chip; one grid overlaps the two and
+// drops a launch boundary (round-1 A/B, profiles/r01_final8/ab_pack.txt).  Surplus x blocks of the
+// shorter pass return at once (block-uniform, before pack_body's barrier).
+__global__ __launch_bounds__(256) void pack_both_kernel(BuildParams P) {
+    if (blockIdx.z == 0) {
+        if ((int)blockIdx.x < 2 * P.n_mt) pack_body<false>(P.f1, P, P.ex1, const_cast<char*>(P.pk1));
+    } else if ((int)blockIdx.x < 2 * P.n_nt) {
+        pack_body<true>(P.f2, P, P.ex2, const_cast<char*>(P.pk2));
+    }
 }
 
-// Epilogue (all threads; contains barriers).  Cs = scaled C-tile rows ([m][n], stride CS,
-// n = ty*16 + tx) of MR of the block's queries (all 128, or one half of them).  Level 0: 4 whole tiles per query (two 256-byte pieces), 32 float4 per query.
-// Pooling: thread (query m, 8x8 block blk) reduces in registers 8x8 -> 4x4 -> 2x2 -> 1, each level
-// from the rounded previous one, parks levels 1-3 in LDS, then level 1 leaves as one whole tile
-// per query, level 2 as two 16-byte rows, level 3 as 8 bytes.  Tiles beyond a level's padded
-// extent are skipped; padding cells inside a tile are written but never read.
-template <int MR, bool NTS>
+// ============================================================================================
+// fp32 GEMM (ecorr_build).  Block tile 128 queries x one 8 x 16 (or 4 x 32 band) target block,
+// K staged 16 deep; 4 waves of 64 x 64 = 2 x 2 v_mfma_f32_32x32x2_f32 tiles, 3 blocks per CU.
+// GLDS: the K chunks go global -> LDS directly (buffer_load_dwordx4 ... lds, whose range check
+// zero-fills the padding) through 3 buffers with two chunks in flight; otherwise (ragged shapes,
+// operands beyond the 31-bit buffer range) float4 / scalar register staging, double-buffered.
+// The C tile passes through LDS in two 64-query halves; the epilogue pools each (query, 8 x 8
+// block) in registers and leaves as whole tiles (levels 0-1) and row pieces (levels 2-3).
+// ============================================================================================
+constexpr int BM = 128;             // queries per block tile
+constexpr int BN = TBH * TBW;       // 128 targets
+constexpr int NT = 256;             // threads
+constexpr int KB = 16;              // K chunk
+constexpr int MR = BM / 2;          // C-tile rows per half
+constexpr int CS = BN + 4;          // C-tile LDS row stride (floats): conflict-free ds_read_b128
+constexpr int P1S = 36, P2S = 12;   // LDS per-query strides of the pooled staging (conflict-free)
+constexpr int FNBUF = 3;
+constexpr int FSM = (FNBUF * KB * (BM + BN) > MR * CS) ? FNBUF * KB * (BM + BN) : MR * CS;
+
+template <typename V>
+__device__ __forceinline__ void st_nt(V* p, V v) { __builtin_nontemporal_store(v, p); }
+
+struct TileCoord { int b, m0, ty0, tx0, band; };
+
+// Epilogue of a regular tile (all threads; contains barriers).  Cs = scaled C-tile rows ([m][n],
+// stride CS, n = ty*16 + tx) of MR of the block's queries starting at mlo.  Level 0: 4 whole tiles
+// per query; pooling: thread (query m, 8 x 8 block blk) reduces in registers 8x8 -> 4x4 -> 2x2 ->
+// 1, each level from the rounded previous one, parks levels 1-3 in LDS, then level 1 leaves as
+// one whole tile per query, level 2 as two 16-byte rows, level 3 as single pixels.
 __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& tc, float* Cs, int tid, int mlo) {
-    // Cs holds C-tile rows [mlo, mlo + MR) of the block's 128 queries
     const int64_t row0 = (int64_t)tc.b * P.q_count + tc.m0 + mlo;
     const int mvalid = min(MR, P.q_count - tc.m0 - mlo);
     {   // level 0
@@ -136,10 +631,10 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
             const int m = idx >> 5, rem = idx & 31;
             const int trl = rem >> 4, tcl = (rem >> 3) & 1, j = rem & 7;
             const int tr = tr0 + trl, tcc = tc0 + tcl;
-            if (m < mvalid && tr < nty && tcc < ntx && P.dev_skip_epilogue != 2) {
+            if (m < mvalid && tr < nty && tcc < ntx) {
                 const floatx4 v = *reinterpret_cast<const floatx4*>(
                     Cs + m * CS + (trl * 4 + (j >> 1)) * TBW + tcl * 8 + (j & 1) * 4);
-                st<NTS>(reinterpret_cast<floatx4*>(P.lvl[0] + (row0 + m) * P.lsz[0] + (tr * ntx + tcc) * kTile + 4 * j), v);
+                st_nt(reinterpret_cast<floatx4*>(P.lvl[0] + (row0 + m) * P.lsz[0] + (tr * ntx + tcc) * kTile + 4 * j), v);
             }
         }
     }
@@ -191,55 +686,27 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
                 const int idx = tid + NT * s;
                 const int mm = idx >> 3, j = idx & 7;
                 if (mm < mvalid)
-                    st<NTS>(reinterpret_cast<floatx4*>(base + (row0 + mm) * P.lsz[1] + 4 * j),
-                            *reinterpret_cast<const floatx4*>(S1 + mm * P1S + 4 * j));
+                    st_nt(reinterpret_cast<floatx4*>(base + (row0 + mm) * P.lsz[1] + 4 * j),
+                          *reinterpret_cast<const floatx4*>(S1 + mm * P1S + 4 * j));
             }
         }
     }
-    if (P.fused_levels >= 3 && tid < 2 * MR && P.dev_skip_epilogue != -1 && P.dev_skip_epilogue != -4) {   // level 2: rows ty0/4 + {0,1}, cols tx0/4 .. +3
+    if (P.fused_levels >= 3 && tid < 2 * MR) {   // level 2: rows ty0/4 + {0,1}, cols tx0/4 .. +3
         const int mm = tid >> 1, y = tid & 1;
         if (mm < mvalid) {
             const float* src = S2 + mm * P2S + y * 4;
-            float* img = P.lvl[2] + (row0 + mm) * P.lsz[2];
-            if (P.lntx[2] > 0) {
-                const int tr = tc.ty0 / 16, tcc = tc.tx0 / 32;
-                if (tr < P.lnty[2] && tcc < P.lntx[2]) {
-                    const int r = ((tc.ty0 / 4) & 3) + y, c0 = (tc.tx0 / 4) & 7;
-                    *reinterpret_cast<floatx4*>(img + (tr * P.lntx[2] + tcc) * kTile + r * 8 + c0) =
-                        *reinterpret_cast<const floatx4*>(src);
-                }
-            } else {   // compact row-major: no padding cells, so every pixel is range-checked
-                const int r = tc.ty0 / 4 + y, c0 = tc.tx0 / 4;
-                if (r < P.lh[2])
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (c0 + j < P.lw[2]) img[r * P.lw[2] + c0 + j] = src[j];
+            for (int j = 0; j < 4; ++j) {
+                float* p = level_px(P, 2, row0 + mm, tc.ty0 / 4 + y, tc.tx0 / 4 + j);
+                if (p) *p = src[j];
             }
         }
     }
-    if (P.fused_levels >= 4 && tid < MR && tid < mvalid && P.dev_skip_epilogue != -1 && P.dev_skip_epilogue != -3) {   // level 3: row ty0/8, cols tx0/8 .. +1
-        const float* src = S3 + tid * 2;
-        float* img = P.lvl[3] + (row0 + tid) * P.lsz[3];
-        if (P.lntx[3] > 0) {
-            const int tr = tc.ty0 / 32, tcc = tc.tx0 / 64;
-            if (tr < P.lnty[3] && tcc < P.lntx[3]) {
-                const int r = (tc.ty0 / 8) & 3, c0 = (tc.tx0 / 8) & 7;
-                *reinterpret_cast<floatx2*>(img + (tr * P.lntx[3] + tcc) * kTile + r * 8 + c0) =
-                    *reinterpret_cast<const floatx2*>(src);
-            }
-        } else {
-            const int r = tc.ty0 / 8, c0 = tc.tx0 / 8;
-            if (r < P.lh[3]) {
-                float* d = img + r * P.lw[3] + c0;
-                // both pixels in range and 8-byte aligned: one 8-byte store instead of two scalars
-                // (ECORR_BUILD_SKIP_EPILOGUE=-5 keeps the scalars, A/B only)
-                if (c0 + 1 < P.lw[3] && (reinterpret_cast<uintptr_t>(d) & 7) == 0 && P.dev_skip_epilogue != -5) {
-                    *reinterpret_cast<floatx2*>(d) = *reinterpret_cast<const floatx2*>(src);
-                } else {
-                    if (c0 < P.lw[3]) d[0] = src[0];
-                    if (c0 + 1 < P.lw[3]) d[1] = src[1];
-                }
-            }
+    if (P.fused_levels >= 4 && tid < MR && tid < mvalid) {   // level 3: row ty0/8, cols tx0/8 .. +1
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            float* p = level_px(P, 3, row0 + tid, tc.ty0 / 8, tc.tx0 / 8 + j);
+            if (p) *p = S3[tid * 2 + j];
         }
     }
 }
@@ -247,8 +714,7 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
 // Epilogue of a band tile (4 target rows x 32 cols; n = ty*32 + tx).  Level 0: one tile row of
 // 4 tiles per query.  Pooling: thread (query m, 4x8 block blk = 0..3) reduces 4x8 -> 2x4 -> 1x2 in
 // registers (the reference's order, from the rounded previous level); level 1 leaves as two 8-float
-// rows of two tiles, level 2 as one 8-float row.  No level-3 pixel draws on these rows.
-template <int MR, bool NTS>
+// rows of two tiles, level 2 as single pixels.  No level-3 pixel draws on these rows.
 __device__ __forceinline__ void epilogue_band(const BuildParams& P, const TileCoord& tc, float* Cs, int tid, int mlo) {
     const int64_t row0 = (int64_t)tc.b * P.q_count + tc.m0 + mlo;
     const int mvalid = min(MR, P.q_count - tc.m0 - mlo);
@@ -260,9 +726,9 @@ __device__ __forceinline__ void epilogue_band(const BuildParams& P, const TileCo
             const int idx = tid + NT * s;
             const int m = idx >> 5, rem = idx & 31;
             const int tcl = rem >> 3, j = rem & 7;
-            if (m < mvalid && tc0 + tcl < ntx && P.dev_skip_epilogue != 2) {
+            if (m < mvalid && tc0 + tcl < ntx) {
                 const floatx4 v = *reinterpret_cast<const floatx4*>(Cs + m * CS + (j >> 1) * 32 + tcl * 8 + (j & 1) * 4);
-                st<NTS>(reinterpret_cast<floatx4*>(P.lvl[0] + (row0 + m) * P.lsz[0] + (tr * ntx + tc0 + tcl) * kTile + 4 * j), v);
+                st_nt(reinterpret_cast<floatx4*>(P.lvl[0] + (row0 + m) * P.lsz[0] + (tr * ntx + tc0 + tcl) * kTile + 4 * j), v);
             }
         }
     }
@@ -315,104 +781,57 @@ __device__ __forceinline__ void epilogue_band(const BuildParams& P, const TileCo
                 const int mm = idx >> 3, t = idx & 7;
                 const int y = t >> 2, tcl = (t >> 1) & 1, hf = t & 1;
                 if (mm < mvalid && tc0 + tcl < P.lntx[1])
-                    st<NTS>(reinterpret_cast<floatx4*>(P.lvl[1] + (row0 + mm) * P.lsz[1] +
-                                                       (tr * P.lntx[1] + tc0 + tcl) * kTile + y * 8 + hf * 4),
-                            *reinterpret_cast<const floatx4*>(S1 + mm * P1S + y * 16 + tcl * 8 + hf * 4));
+                    st_nt(reinterpret_cast<floatx4*>(P.lvl[1] + (row0 + mm) * P.lsz[1] +
+                                                     (tr * P.lntx[1] + tc0 + tcl) * kTile + y * 8 + hf * 4),
+                          *reinterpret_cast<const floatx4*>(S1 + mm * P1S + y * 16 + tcl * 8 + hf * 4));
             }
         }
     }
-    if (P.fused_levels >= 3 && tid < 2 * MR && P.dev_skip_epilogue != -1 && P.dev_skip_epilogue != -4) {   // level 2: row ty0/4, cols tx0/4 .. +7
+    if (P.fused_levels >= 3 && tid < 2 * MR) {   // level 2: row ty0/4, cols tx0/4 .. +7
         const int mm = tid >> 1, hf = tid & 1;
         if (mm < mvalid) {
             const float* src = S2 + mm * P2S + hf * 4;
-            float* img = P.lvl[2] + (row0 + mm) * P.lsz[2];
-            const int r = tc.ty0 / 4, c0 = tc.tx0 / 4 + hf * 4;
-            if (P.lntx[2] > 0) {
-                const int tr = r / 4, tcc = c0 / 8;
-                if (tr < P.lnty[2] && tcc < P.lntx[2])
-                    *reinterpret_cast<floatx4*>(img + (tr * P.lntx[2] + tcc) * kTile + (r & 3) * 8 + (c0 & 7)) =
-                        *reinterpret_cast<const floatx4*>(src);
-            } else if (r < P.lh[2]) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (c0 + j < P.lw[2]) img[r * P.lw[2] + c0 + j] = src[j];
+            for (int j = 0; j < 4; ++j) {
+                float* p = level_px(P, 2, row0 + mm, tc.ty0 / 4, tc.tx0 / 4 + hf * 4 + j);
+                if (p) *p = src[j];
             }
         }
     }
 }
 
-// KB = K chunk depth; HALF = C tile handled in two 64-query halves.  KB = 16 + HALF needs 34 KB of
-// LDS and <= 168 VGPRs, so 3 blocks (3 waves per SIMD) share a CU; KB = 32 uses 67.5 KB (2 blocks).
-// (A/B: v_mfma_f32_16x16x4_f32 tiles, bitwise the same result, ran 1% slower than 32x32x2.)
-//
-// GLDS: the K chunks go global -> LDS directly (buffer_load_dwordx4 ... lds, whose range check
-// zero-fills the padding) through 3 LDS buffers with two chunks in flight: each wave waits for its
-// own copies of chunk kc with a counted vmcnt, one raw barrier publishes them, and chunk kc + 2
-// is issued into the buffer chunk kc - 1 was read from.  No staging registers, no ds_write pass,
-// one barrier per chunk.  Needs VEC and byte offsets below 2^31 (launch_build checks).
-// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt fields at their "don't wait" maxima), N < 16
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N < 16, "vmcnt field");
-    __builtin_amdgcn_s_waitcnt(N | (7 << 4) | (15 << 8));
-}
-
-// SPLIT: the fp32 operands are split into f16 hi + lo per fragment (split_f16, per-pixel
-// power-of-two scales from fmap_exp_kernel) and each 16-deep K chunk runs 3 v_mfma_f32_32x32x16_f16
-// per 32x32 tile (lo*hi, hi*lo, hi*hi; lo*lo is below fp32 rounding) instead of 8 fp32 MFMAs:
-// 3 x 32 vs 8 x 64 matrix-core cycles.  The fragment reads are the fp32 path's: lane (r, h) takes
-// k = 2j + h as element j, the same permutation on both operands.  Normwise error vs fp64 is
-// below the fp32 path's; the result is scaled back by 2^-(e1+e2) exactly.
-//
-// PK (split mode, default): the operands arrive pre-split by pack_kernel as 8-KB panels (one per
-// 128-pixel tile and 16-deep K chunk) laid out in MFMA-fragment order, so LDS-DMA copies them
-// verbatim and each fragment is ONE lane-linear ds_read_b128: no VALU work in the K loop, no zero
-// fill (the panels carry their padding).  The MFMAs take the fmap2 fragment as their A operand,
-// so the accumulators hold C^T and reach the LDS C tile as 16-byte stores.
-// ABL (A/B ablation of the pipelined PK loop only, output invalid; ECORR_BUILD_ABL): 5 no MFMA,
-// 6 no fragment reads, 7 no barrier, 8 no chunk copies -- each also without the epilogue.
-template <bool VEC, int KB, bool HALF, bool NTS, int GBUF = 0, bool SPLIT = false, bool PK = false, int ABL = 0>
-__global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) {
-    static_assert(!PK || (SPLIT && KB == 16 && GBUF > 0), "PK: split mode, 16-deep panels, LDS-DMA");
-    constexpr int MR = HALF ? BM / 2 : BM;
-    constexpr int AS = BM, BSS = BN;   // LDS row strides
-    constexpr int NLD = (KB * BM / 4) / NT;   // float4 of A (and of B) per thread per chunk
-    constexpr bool GLDS = GBUF > 0;
-    constexpr int NBUF = GLDS ? GBUF : 2;   // GLDS: chunks kc .. kc + NBUF - 2 in flight
-    static_assert(!GLDS || (VEC && NLD >= 1 && NBUF >= 3 && 2 * NLD * (NBUF - 2) < 16),
-                  "GLDS: vector path, whole copies per wave, counted vmcnt in range");
-    // ALL LDS in this one array: a second __shared__ object can make hipcc wait vmcnt(0) before
-    // every ds_read while a buffer_load ... lds is in flight (cdna_hip_programming.md trap 4(a))
-    constexpr int SM = smem_floats(KB, MR, AS, BSS, NBUF);
-    __shared__ __attribute__((aligned(16))) float smem[SM + (SPLIT ? BM + BN : 0)];
+// VEC: float4 operand loads (W and q_count multiples of 4, 16-byte aligned fmaps); GLDS: LDS-DMA
+// staging (needs VEC and byte offsets below 2^31).  A/B record: LDS-DMA 2.4-4% faster than
+// register staging; 16x16x4 tiles 1% slower than 32x32x2; KB = 32 / 4 blocks per CU / setprio /
+// k-permuted layouts / fragment prefetch all slower.
+template <bool VEC, bool GLDS>
+__global__ __launch_bounds__(NT, 3) void build_kernel(BuildParams P) {
+    constexpr int AS = BM, BSS = BN;           // LDS row strides
+    constexpr int NLD = (KB * BM / 4) / NT;    // float4 of A (and of B) per thread per chunk (2)
+    constexpr int NBUF = GLDS ? FNBUF : 2;
+    static_assert(!GLDS || VEC, "GLDS: vector path");
+    __shared__ __attribute__((aligned(16))) float smem[FSM];
     float* As = smem;                       // [NBUF][KB][AS]
     float* Bs = smem + NBUF * KB * AS;      // [NBUF][KB][BSS]
-    int* exs = reinterpret_cast<int*>(smem + SM);   // SPLIT: exponents of the BM queries, BN targets
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const TileCoord tc = decode_tile(P, xcd_remap(blockIdx.x, gridDim.x));
+    TileCoord tc;
+    {
+        int mt, nt;
+        decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_mt, tc.b, mt, nt);
+        const NTile n = ntile_of(P, nt);
+        tc.m0 = mt * BM;
+        tc.ty0 = n.ty0;
+        tc.tx0 = n.tx0;
+        tc.band = n.band;
+    }
     const int q_end = P.q_count;
     const int H = P.H, W = P.W, D = P.D;
     const int64_t Q = (int64_t)H * W;
     const int64_t QA = P.q_count;
     const float* __restrict__ A = P.f1 + (int64_t)tc.b * D * QA;
     const float* __restrict__ Bm = P.f2 + (int64_t)tc.b * D * Q;
-    if constexpr (SPLIT) {
-        // LDS column n of the B tile is target (y, x) as the loads below map it
-        const int t = threadIdx.x;
-        int e = 0;
-        if (t < BM) {
-            if (tc.m0 + t < P.q_count) e = P.ex1[(int64_t)tc.b * P.q_count + tc.m0 + t];
-        } else {
-            const int n = t - BM, c = n >> 2;
-            const int y = tc.ty0 + (tc.band ? c >> 3 : c >> 2), x = tc.tx0 + 4 * (tc.band ? c & 7 : c & 3) + (n & 3);
-            if (y < P.H && x < P.W) e = P.ex2[(int64_t)tc.b * Q + (int64_t)y * P.W + x];
-        }
-        exs[t] = e;
-        __syncthreads();
-    }
 
-    // ---- global -> register staging: NLD float4 of A and of B per thread per K chunk ----
     floatx4 ra[NLD], rb[NLD];
     auto load_chunk = [&](int k0) {
 #pragma unroll
@@ -470,75 +889,9 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
     const int arow = lane >> 5, acol = lane & 31;
     const int nk = (D + KB - 1) / KB;
 
-    float sa0 = 1.f, sa1 = 1.f, sb0 = 1.f, sb1 = 1.f;
-    if constexpr (SPLIT && !PK) {
-        sa0 = exp2i(exs[wm * 64 + acol]);
-        sa1 = exp2i(exs[wm * 64 + 32 + acol]);
-        sb0 = exp2i(exs[BM + wn * 64 + acol]);
-        sb1 = exp2i(exs[BM + wn * 64 + 32 + acol]);
-    }
-
     auto mfma_chunk = [&](int buf) {
         const float* as = As + buf * KB * AS + wm * 64 + acol;
         const float* bs = Bs + buf * KB * BSS + wn * 64 + acol;
-        if constexpr (PK) {
-            // panel: [32-row group][hi h0 | hi h1 | lo h0 | lo h1][32 rows][8 halves]
-            const char* ap = reinterpret_cast<const char*>(As + buf * KB * AS) + wm * 4096 + lane * 16;
-            const char* bp = reinterpret_cast<const char*>(Bs + buf * KB * BSS) + wn * 4096 + lane * 16;
-            const halfx8 a0h = *reinterpret_cast<const halfx8*>(ap);
-            const halfx8 a0l = *reinterpret_cast<const halfx8*>(ap + 1024);
-            const halfx8 a1h = *reinterpret_cast<const halfx8*>(ap + 2048);
-            const halfx8 a1l = *reinterpret_cast<const halfx8*>(ap + 3072);
-            const halfx8 b0h = *reinterpret_cast<const halfx8*>(bp);
-            const halfx8 b0l = *reinterpret_cast<const halfx8*>(bp + 1024);
-            const halfx8 b1h = *reinterpret_cast<const halfx8*>(bp + 2048);
-            const halfx8 b1l = *reinterpret_cast<const halfx8*>(bp + 3072);
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0h, a0l, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1h, a0l, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0h, a1l, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1h, a1l, acc[1][1], 0, 0, 0);
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0l, a0h, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1l, a0h, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0l, a1h, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1l, a1h, acc[1][1], 0, 0, 0);
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0h, a0h, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1h, a0h, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b0h, a1h, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b1h, a1h, acc[1][1], 0, 0, 0);
-            return;
-        }
-        if constexpr (SPLIT) {
-#pragma unroll
-            for (int k16 = 0; k16 < KB; k16 += 16) {
-                float va0[8], va1[8], vb0[8], vb1[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int ro = k16 + 2 * j + arow;
-                    va0[j] = as[ro * AS];
-                    va1[j] = as[ro * AS + 32];
-                    vb0[j] = bs[ro * BSS];
-                    vb1[j] = bs[ro * BSS + 32];
-                }
-                halfx8 a0h, a0l, a1h, a1l, b0h, b0l, b1h, b1l;
-                split_f16(va0, sa0, a0h, a0l);
-                split_f16(va1, sa1, a1h, a1l);
-                split_f16(vb0, sb0, b0h, b0l);
-                split_f16(vb1, sb1, b1h, b1l);
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0l, b0h, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0l, b1h, acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l, b0h, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l, b1h, acc[1][1], 0, 0, 0);
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b0l, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b1l, acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b0l, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b1l, acc[1][1], 0, 0, 0);
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b0h, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h, b1h, acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b0h, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h, b1h, acc[1][1], 0, 0, 0);
-            }
-            return;
-        }
 #pragma unroll
         for (int kk = 0; kk < KB; kk += 2) {
             const int ro = kk + arow;
@@ -564,29 +917,8 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
         const int y = tc.ty0 + (tc.band ? c >> 3 : c >> 2), x = tc.tx0 + 4 * (tc.band ? c & 7 : c & 3);
         const bool aok = m < q_end, bok = y < H && x < W;
         const int abase = m * 4, bbase = (y * W + x) * 4;
-        // PK: this tile's panels, chunk-major (pack_kernel layout)
-        const int dc = (D + 15) / 16;
-        const char* pa = PK ? P.pk1 + ((int64_t)tc.b * P.n_mt + tc.mt) * dc * 8192 : nullptr;
-        const char* pb = PK ? P.pk2 + ((int64_t)tc.b * P.n_nt + tc.nt) * dc * 8192 : nullptr;
-        const __amdgpu_buffer_rsrc_t rpa =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pa), 0, dc * 8192, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rpb =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pb), 0, dc * 8192, 0x00020000);
         auto issue = [&](int kc) {
             const int buf = kc % NBUF;
-            if constexpr (PK) {
-#pragma unroll
-                for (int i = 0; i < NLD; ++i) {
-                    const int slot = i * NT + wave * 64;   // wave-uniform 16-byte slot of this copy
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                        rpa, (__attribute__((address_space(3))) void*)(As + buf * KB * AS + 4 * slot), 16,
-                        kc * 8192 + (slot + lane) * 16, 0, 0, 0);
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                        rpb, (__attribute__((address_space(3))) void*)(Bs + buf * KB * BSS + 4 * slot), 16,
-                        kc * 8192 + (slot + lane) * 16, 0, 0, 0);
-                }
-                return;
-            }
 #pragma unroll
             for (int i = 0; i < NLD; ++i) {
                 const int kk = 2 * wave + 8 * i;   // wave-uniform first row of this copy
@@ -600,101 +932,17 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
                     bok && kin ? bbase + k * (int)Q * 4 : OOB, 0, 0, 0);
             }
         };
-        if constexpr (PK) {
-            if (P.dev_pk_pipe && nk % 2 == 0) {
-                // software-pipelined (even chunk counts): chunk kc + 1's fragments are read (after
-                // its barrier) between the lo*hi MFMAs of chunk kc and its hi*lo / hi*hi MFMAs, so
-                // the barrier and the LDS latency hide behind the matrix pipe; two register sets,
-                // loop unrolled by 2
-                auto read_frags = [&](int buf, halfx8 (&f)[8]) {
-                    if constexpr (ABL == 6) return;
-                    const char* ap = reinterpret_cast<const char*>(As + buf * KB * AS) + wm * 4096 + lane * 16;
-                    const char* bp = reinterpret_cast<const char*>(Bs + buf * KB * BSS) + wn * 4096 + lane * 16;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        f[q] = *reinterpret_cast<const halfx8*>(ap + q * 1024);       // a0h a0l a1h a1l
-                        f[4 + q] = *reinterpret_cast<const halfx8*>(bp + q * 1024);   // b0h b0l b1h b1l
-                    }
-                };
-                auto mfma_lohi = [&](const halfx8 (&f)[8]) {
-                    if constexpr (ABL == 5) {
-#pragma unroll
-                        for (int q = 0; q < 8; ++q) asm volatile("" ::"v"(f[q]));
-                        return;
-                    }
-                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[4], f[1], acc[0][0], 0, 0, 0);
-                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[6], f[1], acc[0][1], 0, 0, 0);
-                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[4], f[3], acc[1][0], 0, 0, 0);
-                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[6], f[3], acc[1][1], 0, 0, 0);
-                };
-                auto mfma_rest = [&](const halfx8 (&f)[8]) {
-                    if constexpr (ABL == 5) return;
-                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[5], f[0], acc[0][0], 0, 0, 0);
-                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[7], f[0], acc[0][1], 0, 0, 0);
-                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[5], f[2], acc[1][0], 0, 0, 0);
-                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[7], f[2], acc[1][1], 0, 0, 0);
-                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[4], f[0], acc[0][0], 0, 0, 0);
-                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[6], f[0], acc[0][1], 0, 0, 0);
-                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[4], f[2], acc[1][0], 0, 0, 0);
-                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f[6], f[2], acc[1][1], 0, 0, 0);
-                };
-                // chunk j's buffer is j % NBUF; a chunk is issued into the buffer whose reads the
-                // preceding barrier retired.  Exactly one chunk stays in flight at every wait:
-                // chunks past the end are still issued (their offsets fall outside the panel range,
-                // so they land as zeros in a retired buffer) and the last advance reads such a
-                // chunk, which keeps the loop free of branches (and of conservative waitcnts)
-                auto advance = [&](int& issued, int j, halfx8 (&f)[8]) {
-                    // vmcnt(2 NLD (NBUF - 2)): chunk j landed, the NBUF - 2 after it may fly;
-                    // lgkmcnt(0): this wave's reads of chunk j - 1 (half of them not yet consumed
-                    // by an MFMA) are done before the barrier hands their buffer to chunk
-                    // j + NBUF - 1
-                    static_assert(2 * NLD * (NBUF - 2) < 16, "vmcnt field");
-                    __builtin_amdgcn_s_waitcnt((2 * NLD * (NBUF - 2)) | (7 << 4));
-                    if constexpr (ABL != 7) __builtin_amdgcn_s_barrier();
-                    if constexpr (ABL != 8) issue(issued);
-                    ++issued;
-                    read_frags(j % NBUF, f);
-                };
-                halfx8 fa[8], fb[8];
-                if constexpr (ABL == 6) {
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) fa[q] = fb[q] = halfx8{};
-                }
-                int issued = 0;
-                while (issued < NBUF - 1) issue(issued++);
-                advance(issued, 0, fa);
-                for (int kc = 0; kc < nk; kc += 2) {
-                    mfma_lohi(fa);
-                    advance(issued, kc + 1, fb);
-                    mfma_rest(fa);
-                    mfma_lohi(fb);
-                    advance(issued, kc + 2, fa);
-                    mfma_rest(fb);
-                }
-                wait_vmcnt<0>();
-                goto chunks_done;
-            }
-        }
         for (int kc = 0; kc < NBUF - 1 && kc < nk; ++kc) issue(kc);
         for (int kc = 0; kc < nk; ++kc) {
-            // this wave's copies of chunk kc have landed (those of the later issued chunks may
-            // still fly: 2 NLD copies each) ...
-            const int after = min(nk, kc + NBUF - 1) - (kc + 1);
-            static_assert(NBUF <= 6, "wait ladder");
-            switch (after) {
-                case 0: wait_vmcnt<0>(); break;
-                case 1: wait_vmcnt<2 * NLD * (NBUF > 2 ? 1 : 0)>(); break;
-                case 2: wait_vmcnt<2 * NLD * (NBUF > 3 ? 2 : 0)>(); break;
-                case 3: wait_vmcnt<2 * NLD * (NBUF > 4 ? 3 : 0)>(); break;
-                default: wait_vmcnt<2 * NLD * (NBUF > 5 ? 4 : 0)>(); break;
-            }
+            // this wave's copies of chunk kc have landed (those of chunk kc + 1 may still fly) ...
+            if (kc + 1 < nk) wait_vm<2 * NLD, false>();
+            else wait_vm<0, false>();
             // ... and every wave's have once all passed this barrier, which also retires the
-            // reads of chunk kc - 1, whose buffer chunk kc + NBUF - 1 now overwrites
+            // reads of chunk kc - 1, whose buffer chunk kc + 2 now overwrites
             __builtin_amdgcn_s_barrier();
-            if (kc + NBUF - 1 < nk && P.dev_skip_epilogue < 3) issue(kc + NBUF - 1);
+            if (kc + NBUF - 1 < nk) issue(kc + NBUF - 1);
             mfma_chunk(kc % NBUF);
         }
-    chunks_done:
         __syncthreads();   // the C tile aliases the chunk buffers
     } else {
         load_chunk(0);
@@ -702,72 +950,44 @@ __global__ __launch_bounds__(NT, HALF ? 3 : 2) void build_kernel(BuildParams P) 
         __syncthreads();
         for (int kc = 0; kc < nk; ++kc) {
             const int buf = kc & 1;
-            if (kc + 1 < nk && P.dev_skip_epilogue < 3) load_chunk((kc + 1) * KB);
+            if (kc + 1 < nk) load_chunk((kc + 1) * KB);
             mfma_chunk(buf);
-            if (kc + 1 < nk && P.dev_skip_epilogue < 4) store_chunk(buf ^ 1);
+            if (kc + 1 < nk) store_chunk(buf ^ 1);
             __syncthreads();
         }
     }
 
-    // ---- scaled accumulators -> LDS C tile [m][n]; C/D map: col = lane&31,
-    //      row = (reg&3) + 8*(reg>>2) + 4*(lane>>5) ----
+    // ---- scaled accumulators -> LDS C tile [m][n] in two 64-query halves; C/D map:
+    //      col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5) ----
     float* Cs = smem;
 #pragma unroll
-    for (int half = 0; half < (HALF ? 2 : 1); ++half) {
-        if (!HALF || wm == half) {
-            const int mb = HALF ? 0 : wm * 64;
+    for (int half = 0; half < 2; ++half) {
+        if (wm == half) {
             // one uniform branch on the scale mode around the whole tile (a per-element select
             // had the compiler emit an IEEE division next to every element's multiply)
             auto write_c = [&](auto scaled) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        if constexpr (PK) {
-                            // PK tiles are C^T (targets on the rows, queries on the lanes): each
-                            // lane's 4 consecutive rows are 4 consecutive targets of one query, one
-                            // 16-byte LDS store (row stride 132: conflict-free)
-                            const int m = mb + i * 32 + acol;
-                            const int ea = exs[(HALF ? half * 64 : 0) + m];
+                    for (int j = 0; j < 2; ++j)
 #pragma unroll
-                            for (int g4 = 0; g4 < 4; ++g4) {
-                                const int n = wn * 64 + j * 32 + 8 * g4 + 4 * arow;
-                                floatx4 v;
-#pragma unroll
-                                for (int t = 0; t < 4; ++t) v[t] = scaled(acc[i][j][4 * g4 + t], ea + exs[BM + n + t]);
-                                *reinterpret_cast<floatx4*>(Cs + m * CS + n) = v;
-                            }
-                        } else {
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) {
-                                const int m = mb + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
-                                const int n = wn * 64 + j * 32 + acol;
-                                const int e = SPLIT ? exs[(HALF ? half * 64 : 0) + m] + exs[BM + n] : 0;
-                                Cs[m * CS + n] = scaled(acc[i][j][r], e);
-                            }
+                        for (int r = 0; r < 16; ++r) {
+                            const int m = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * arow;
+                            const int n = wn * 64 + j * 32 + acol;
+                            Cs[m * CS + n] = scaled(acc[i][j][r]);
                         }
-                    }
             };
-            if (P.scale_is_mul) {
-                // v * 2^-(e1+e2) * 2^-s as one exact scaling (unless subnormal) when 1/sqrt(D) = 2^-s
-                if constexpr (SPLIT) write_c([&](float v, int e) { return ldexpf(v, -(e + P.scale_shift)); });
-                else write_c([&](float v, int) { return __fmul_rn(v, P.scale); });
-            } else {
-                write_c([&](float v, int e) {
-                    // SPLIT: undo the 2^(e1+e2) operand scaling (exact unless subnormal), then divide
-                    return __fdiv_rn(SPLIT ? ldexpf(v, -e) : v, P.scale);
-                });
-            }
+            if (P.scale_is_mul) write_c([&](float v) { return __fmul_rn(v, P.scale); });
+            else write_c([&](float v) { return __fdiv_rn(v, P.scale); });
         }
         __syncthreads();
-        if (ABL || P.dev_skip_epilogue == 1 || P.dev_skip_epilogue >= 3) continue;
-        if (tc.band) epilogue_band<MR, NTS>(P, tc, Cs, tid, half * MR);
-        else epilogue<MR, NTS>(P, tc, Cs, tid, half * MR);
-        if (HALF && half == 0) __syncthreads();   // half 0 fully consumed before half 1 overwrites Cs
+        if (tc.band) epilogue_band(P, tc, Cs, tid, half * MR);
+        else epilogue(P, tc, Cs, tid, half * MR);
+        if (half == 0) __syncthreads();   // half 0 fully consumed before half 1 overwrites Cs
     }
 }
 
-// Levels beyond the 3 fused ones (num_levels > 4): plain 2x2 floor-mode pooling, tiled in and
+// Levels beyond the 4 fused ones (num_levels > 4): plain 2x2 floor-mode pooling, tiled in and
 // out, one thread per output pixel.  Not on the E-RAFT path (num_levels = 4, eraft.py:50).
 __global__ __launch_bounds__(256) void pool2_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                     int64_t rows, int h, int w, int ntx_in, int64_t sz_in,
@@ -785,157 +1005,20 @@ __global__ __launch_bounds__(256) void pool2_kernel(const float* __restrict__ in
     }
 }
 
-// Split-mode exponent pass: ex[b][n] = 15 - E with max_d |x[b][d][n]| = f 2^E, f in [0.5, 1)
-// (so the pixel's largest scaled value lies in [2^14, 2^15)); 0 for all-zero or non-finite maxima
-// (NaN inputs propagate through the GEMM as in the reference).  x: [B][D][N].  Block = 64 pixels
-// x 4 channel groups (coalesced 256-byte rows per wave), grid (ceil(N / 64), B).
-__global__ __launch_bounds__(256) void fmap_exp_kernel(const float* __restrict__ x, int D, int64_t N,
-                                                       int* __restrict__ ex) {
-    __shared__ float red[4][64];
-    const int b = blockIdx.y, l = threadIdx.x & 63, g = threadIdx.x >> 6;
-    const int64_t n = (int64_t)blockIdx.x * 64 + l;
-    float m = 0.f;
-    if (n < N) {
-        const float* p = x + (int64_t)b * D * N + n;
-        for (int d = g; d < D; d += 4) m = fmaxf(m, fabsf(p[(int64_t)d * N]));
-    }
-    red[g][l] = m;
-    __syncthreads();
-    if (g == 0 && n < N) {
-        m = fmaxf(fmaxf(red[0][l], red[1][l]), fmaxf(red[2][l], red[3][l]));
-        int E = 0;
-        frexpf(m, &E);
-        int e = (m > 0.f && m <= 3.4028235e38f) ? 15 - E : 0;
-        e = e < -126 ? -126 : (e > 126 ? 126 : e);
-        ex[(int64_t)b * N + n] = e;
-    }
-}
-
-// Split-mode operand pass (PK build): per pixel, the power-of-two exponent of fmap_exp_kernel and
-// the f16 hi/lo split of all D values, written as the build's 8-KB panels: panel (tile, chunk) =
-// [32-row group g][hi k0-7 | hi k8-15 | lo k0-7 | lo k8-15][row r][8 halves], i.e. the
-// v_mfma_f32_32x32x16_f16 operand of lane (r, h) is the 16 bytes at g*2048 + part*1024 + lane*16.
-// Tile positions without a pixel (ragged edges) and k >= D are written as zeros.
-// ISB = 0: fmap1 slab, tile = 128 consecutive queries; ISB = 1: fmap2, tile = the build's 8 x 16
-// (or 4 x 32 band) target block in its LDS column order.  Block = 64 positions x 4 chunk
-// quarters; grid (2 * tiles, B).  The second pass re-reads the block's 64 KB (L2 / MALL hits).
-template <bool ISB>
-__device__ __forceinline__ void pack_body(const float* __restrict__ x, const BuildParams& P, int* __restrict__ ex,
-                                          char* __restrict__ pack) {
-    __shared__ float red[4][64];
-    const int b = blockIdx.y, tile = blockIdx.x >> 1, pos = (blockIdx.x & 1) * 64 + (threadIdx.x & 63);
-    const int qtr = threadIdx.x >> 6, D = P.D, dc = (D + 15) / 16;
-    const int64_t N = ISB ? (int64_t)P.H * P.W : (int64_t)P.q_count;
-    int64_t pix = -1;
-    if (!ISB) {
-        const int64_t p = (int64_t)tile * BM + pos;
-        if (p < P.q_count) pix = p;
-    } else {
-        int y, xx;
-        if (tile < P.n_reg) {
-            y = (tile / P.n_ntx) * TBH + (pos >> 4);
-            xx = (tile % P.n_ntx) * TBW + (pos & 15);
-        } else {
-            y = P.band_y0 + (pos >> 5);
-            xx = (tile - P.n_reg) * 32 + (pos & 31);
-        }
-        if (y < P.H && xx < P.W) pix = (int64_t)y * P.W + xx;
-    }
-    const float* px = x + (int64_t)b * D * N + (pix < 0 ? 0 : pix);
-    // D <= 256 (E-RAFT: 256): this thread's <= 4 chunks stay in registers between the max and the
-    // split, so the operand is read once; larger D re-reads it in the second pass
-    constexpr int CPT = 4;
-    const bool regs = dc <= 4 * CPT;
-    float v[CPT][16];
-    float m = 0.f;
-    if (regs) {
-#pragma unroll
-        for (int i = 0; i < CPT; ++i)
-#pragma unroll
-            for (int kk = 0; kk < 16; ++kk) {
-                const int k = (qtr + 4 * i) * 16 + kk;
-                v[i][kk] = (pix >= 0 && k < D) ? px[(int64_t)k * N] : 0.f;
-                m = fmaxf(m, fabsf(v[i][kk]));
-            }
-    } else if (pix >= 0) {
-        for (int k = qtr * 16; k < D; k += 64)
-#pragma unroll 4
-            for (int kk = 0; kk < 16 && k + kk < D; ++kk) m = fmaxf(m, fabsf(px[(int64_t)(k + kk) * N]));
-    }
-    red[qtr][threadIdx.x & 63] = m;
-    __syncthreads();
-    const int l = threadIdx.x & 63;
-    m = fmaxf(fmaxf(red[0][l], red[1][l]), fmaxf(red[2][l], red[3][l]));
-    int E = 0;
-    frexpf(m, &E);
-    int e = (m > 0.f && m <= 3.4028235e38f) ? 15 - E : 0;
-    e = e < -126 ? -126 : (e > 126 ? 126 : e);
-    if (qtr == 0 && pix >= 0) ex[(int64_t)b * N + pix] = e;
-    const float s = exp2i(e);
-    const int ntiles = ISB ? P.n_nt : P.n_mt;
-    char* pan = pack + ((int64_t)b * ntiles + tile) * dc * 8192 + (pos >> 5) * 2048 + (pos & 31) * 16;
-    auto put = [&](int c, const float (&w)[16]) {
-        halfx8 h0, l0, h1, l1;
-        split_f16(*reinterpret_cast<const float(*)[8]>(w), s, h0, l0);
-        split_f16(*reinterpret_cast<const float(*)[8]>(w + 8), s, h1, l1);
-        char* p = pan + (int64_t)c * 8192;
-        *reinterpret_cast<halfx8*>(p) = h0;
-        *reinterpret_cast<halfx8*>(p + 512) = h1;
-        *reinterpret_cast<halfx8*>(p + 1024) = l0;
-        *reinterpret_cast<halfx8*>(p + 1536) = l1;
-    };
-    if (regs) {
-#pragma unroll
-        for (int i = 0; i < CPT; ++i)
-            if (qtr + 4 * i < dc) put(qtr + 4 * i, v[i]);
-        return;
-    }
-    for (int c = qtr; c < dc; c += 4) {
-        float w[16];
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) {
-            const int k = c * 16 + kk;
-            w[kk] = (pix >= 0 && k < D) ? px[(int64_t)k * N] : 0.f;
-        }
-        put(c, w);
-    }
-}
-
-template <bool ISB>
-__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, BuildParams P, int* __restrict__ ex,
-                                                   char* __restrict__ pack) {
-    pack_body<ISB>(x, P, ex, pack);
-}
-
-// Both operand passes in ONE launch: grid (2 * max(n_mt, n_nt), B, 2), z = 0 packs fmap1 (slab
-// tiles), z = 1 fmap2 (target blocks).  Neither pass alone fills the chip (1,216 blocks at DSEC
-// B = 16, all resident at once, latency-bound on their 64 loads per thread); one grid overlaps
-// the two and drops a launch boundary: build 0.836 -> 0.826 ms at DSEC B = 16 (rotated A/B,
-// profiles/r01_final8/ab_pack.txt; a 128-VGPR cap for 4 waves per SIMD spills and gains nothing,
-// 0.829).  Surplus x blocks of the shorter pass return at once (block-uniform, before
-// pack_body's barrier).
-__global__ __launch_bounds__(256) void pack_both_kernel(BuildParams P) {
-    if (blockIdx.z == 0) {
-        if ((int)blockIdx.x < 2 * P.n_mt) pack_body<false>(P.f1, P, P.ex1, const_cast<char*>(P.pk1));
-    } else if ((int)blockIdx.x < 2 * P.n_nt) {
-        pack_body<true>(P.f2, P, P.ex2, const_cast<char*>(P.pk2));
-    }
-}
-
 }  // namespace
 
 namespace {
 void tile_counts(BuildParams& P) {
     P.n_ntx = (P.W + TBW - 1) / TBW;
     // 8-row tile rows; a remainder of 1..4 rows (the last 8k + r rows, r <= 4) becomes a band of
-    // 4 x 32 tiles (see TileCoord), a remainder of 5..7 a padded regular tile row
+    // 4 x 32 tiles (see ntile_of), a remainder of 5..7 a padded regular tile row
     const int rem = P.H % TBH;
-    // dev knob for A/B (tools/ab_build.py): ECORR_BUILD_NOBAND=1 pads the remainder instead
-    const bool band = rem > 0 && rem <= 4 && getenv("ECORR_BUILD_NOBAND") == nullptr;
+    const bool band = rem > 0 && rem <= 4;
     P.n_reg = P.n_ntx * (band ? P.H / TBH : (P.H + TBH - 1) / TBH);
     P.band_y0 = (P.H / TBH) * TBH;
     P.n_nt = P.n_reg + (band ? (P.W + 31) / 32 : 0);
-    P.n_mt = (P.q_count + BM - 1) / BM;
+    P.n_mt = (P.q_count + BM - 1) / BM;      // 128-query tiles (fp32 blocks, fmap1 panels)
+    P.n_qt = (P.q_count + SQ - 1) / SQ;      // 256-query tiles (split blocks)
 }
 
 // split workspace: exponents (fmap1 slab, fmap2), then fmap1 and fmap2 panels (256-B aligned)
@@ -945,8 +1028,8 @@ SplitWs split_ws(const BuildParams& P, int B) {
     SplitWs w;
     w.ex2 = (int64_t)B * P.q_count * 4;
     w.pk1 = (w.ex2 + (int64_t)B * P.H * P.W * 4 + 255) & ~(int64_t)255;
-    w.pk2 = w.pk1 + (int64_t)B * P.n_mt * dc * 8192;
-    w.total = w.pk2 + (int64_t)B * P.n_nt * dc * 8192;
+    w.pk2 = w.pk1 + (int64_t)B * P.n_mt * dc * PANEL;
+    w.total = w.pk2 + (int64_t)B * P.n_nt * dc * PANEL;
     return w;
 }
 }  // namespace
@@ -966,9 +1049,6 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
     const int levels = g.levels;
     P.fused_levels = levels < 4 ? levels : 4;
     tile_counts(P);
-    // m-tiles per group of the tile order (dev knob ECORR_BUILD_GM for A/B; default 8)
-    const char* kgm = getenv("ECORR_BUILD_GM");
-    P.gm = kgm && atoi(kgm) > 0 ? atoi(kgm) : 8;
     for (int i = 0; i < 4; ++i) {
         const bool on = i < levels;
         P.lvl[i] = on ? pyramid + g.off[i] : nullptr;
@@ -978,75 +1058,35 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
         P.lnty[i] = on ? g.nty[i] : 0;
         P.lsz[i] = on ? g.sz[i] : 0;
     }
-    const int64_t ntiles = (int64_t)B * P.n_mt * P.n_nt;
-    if (ntiles <= 0 || ntiles > 0x7fffffff) return ECORR_EINVAL;
-    P.n_tiles = (int)ntiles;
-    // dev knob for A/B ablation (tools/ab_build.py): ECORR_BUILD_SKIP_EPILOGUE=1 drops the pyramid
-    // stores (output invalid); unset in production.
-    const char* kskip = getenv("ECORR_BUILD_SKIP_EPILOGUE");
-    // 2: level-0 stores only; 3: + no K-chunk global loads (LDS refilled from stale registers);
-    // 4: + no LDS refill (MFMA + fragment reads only)
-    P.dev_skip_epilogue = kskip ? atoi(kskip) : 0;
-    const bool vec = (P.W % 4 == 0) && (P.q_count % 4 == 0) && ((uintptr_t)P.f1 % 16 == 0) &&
-                     ((uintptr_t)P.f2 % 16 == 0);
     if ((uintptr_t)pyramid % 16 != 0) return ECORR_EINVAL;   // tile stores are 16-byte vectors
-    // dev knob for A/B (tools/ab_build.py): ECORR_BUILD_KB32=1 selects the K=32, full-C-tile,
-    // 2-blocks-per-CU variant
-    const char* kv = getenv("ECORR_BUILD_KB32");
-    const bool kb32 = kv && atoi(kv) == 1;
-    // LDS-DMA staging (3% faster than register staging, tools/ab_build.py) whenever both operands'
-    // byte offsets fit the 31-bit buffer range; dev knob ECORR_BUILD_GLDS=0 selects the register-
-    // staged loop for A/B
-    const char* kg = getenv("ECORR_BUILD_GLDS");
-    const bool glds = !(kg && atoi(kg) == 0) && (int64_t)P.D * P.H * P.W * 4 < 0x7fff0000LL &&
-                      (int64_t)P.D * P.q_count * 4 < 0x7fff0000LL;
-    const dim3 grid((unsigned)ntiles), block(NT);
     if (P.ws) {
-        const int64_t Q = (int64_t)P.H * P.W;
+        // split build: one 128-query tile's panels (dc * 8 KB, the buffer range of the kernel's
+        // per-tile descriptors) always fit 31 bits for D < 2^22
+        const int64_t ntiles = (int64_t)B * P.n_qt * P.n_nt;
+        if (ntiles <= 0 || ntiles > 0x7fffffff || (int64_t)2 * ((P.D + 15) / 16) * PANEL >= 0x7fff0000LL)
+            return ECORR_EINVAL;
         const SplitWs w = split_ws(P, B);
         P.ex1 = reinterpret_cast<int*>(P.ws);
         P.ex2 = reinterpret_cast<int*>(P.ws + w.ex2);
         P.pk1 = P.ws + w.pk1;
         P.pk2 = P.ws + w.pk2;
-        // PK needs one batch item's panels inside the 31-bit buffer range; dev knob
-        // ECORR_BUILD_PK=0 selects the in-loop split (A/B)
-        const char* kp = getenv("ECORR_BUILD_PK");
-        const char* kpp = getenv("ECORR_BUILD_PKPIPE");   // dev knob: 0 = unpipelined PK loop (A/B)
-        P.dev_pk_pipe = !(kpp && atoi(kpp) == 0);
-        const bool pk = !(kp && atoi(kp) == 0) &&
-                        (int64_t)(P.n_mt > P.n_nt ? P.n_mt : P.n_nt) * ((P.D + 15) / 16) * 8192 < 0x7fff0000LL;
-        if (pk) {
-            const char* k2 = getenv("ECORR_BUILD_PACK2");   // dev knob (A/B): 1 = one launch per operand
-            if (k2 && atoi(k2) == 1) {
-                hipLaunchKernelGGL(pack_kernel<false>, dim3((unsigned)(2 * P.n_mt), B), dim3(256), 0, stream, P.f1, P,
-                                   P.ex1, P.ws + w.pk1);
-                hipLaunchKernelGGL(pack_kernel<true>, dim3((unsigned)(2 * P.n_nt), B), dim3(256), 0, stream, P.f2, P,
-                                   P.ex2, P.ws + w.pk2);
-            } else {
-                const int nx = 2 * (P.n_mt > P.n_nt ? P.n_mt : P.n_nt);
-                hipLaunchKernelGGL(pack_both_kernel, dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
-            }
-            const char* ka = getenv("ECORR_BUILD_ABL");   // dev knob: loop ablations (A/B only)
-            switch (ka && P.dev_pk_pipe ? atoi(ka) : 0) {
-                case 5: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true, 5>), grid, block, 0, stream, P); break;
-                case 6: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true, 6>), grid, block, 0, stream, P); break;
-                case 7: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true, 7>), grid, block, 0, stream, P); break;
-                case 8: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true, 8>), grid, block, 0, stream, P); break;
-                default: hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true, true>), grid, block, 0, stream, P);
-            }
-        } else {   // in-loop split: exponents only, fp32 operands staged as in the fp32 build
-            hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((P.q_count + 63) / 64), B), dim3(256), 0, stream,
-                               P.f1, P.D, (int64_t)P.q_count, P.ex1);
-            hipLaunchKernelGGL(fmap_exp_kernel, dim3((unsigned)((Q + 63) / 64), B), dim3(256), 0, stream, P.f2, P.D,
-                               Q, P.ex2);
-            if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true, 0, true>), grid, block, 0, stream, P);
-            else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3, true>), grid, block, 0, stream, P);
-            else hipLaunchKernelGGL((build_kernel<true, 16, true, true, 0, true>), grid, block, 0, stream, P);
-        }
-    } else if (!vec) hipLaunchKernelGGL((build_kernel<false, 16, true, true>), grid, block, 0, stream, P);
-    else if (kb32) hipLaunchKernelGGL((build_kernel<true, 32, false, true>), grid, block, 0, stream, P);
-    else if (glds) hipLaunchKernelGGL((build_kernel<true, 16, true, true, 3>), grid, block, 0, stream, P);
-    else hipLaunchKernelGGL((build_kernel<true, 16, true, true>), grid, block, 0, stream, P);
+        const int nx = 2 * (P.n_mt > P.n_nt ? P.n_mt : P.n_nt);
+        hipLaunchKernelGGL(pack_both_kernel, dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
+        if (P.scale_is_mul) hipLaunchKernelGGL(build_split_kernel<true>, dim3((unsigned)ntiles), dim3(256), 0, stream, P);
+        else hipLaunchKernelGGL(build_split_kernel<false>, dim3((unsigned)ntiles), dim3(256), 0, stream, P);
+    } else {
+        const int64_t ntiles = (int64_t)B * P.n_mt * P.n_nt;
+        if (ntiles <= 0 || ntiles > 0x7fffffff) return ECORR_EINVAL;
+        const bool vec = (P.W % 4 == 0) && (P.q_count % 4 == 0) && ((uintptr_t)P.f1 % 16 == 0) &&
+                         ((uintptr_t)P.f2 % 16 == 0);
+        // LDS-DMA staging whenever both operands' byte offsets fit the 31-bit buffer range
+        const bool glds = vec && (int64_t)P.D * P.H * P.W * 4 < 0x7fff0000LL &&
+                          (int64_t)P.D * P.q_count * 4 < 0x7fff0000LL;
+        const dim3 grid((unsigned)ntiles), block(NT);
+        if (glds) hipLaunchKernelGGL((build_kernel<true, true>), grid, block, 0, stream, P);
+        else if (vec) hipLaunchKernelGGL((build_kernel<true, false>), grid, block, 0, stream, P);
+        else hipLaunchKernelGGL((build_kernel<false, false>), grid, block, 0, stream, P);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ECORR_EHIP - (int)e;
     const int64_t rows = (int64_t)B * P.q_count;

@@ -33,16 +33,14 @@ struct BuildParams {
     char* ws;           // split workspace (build_split_workspace_bytes), null = fp32 build
     int* ex1;
     int* ex2;
-    const char* pk1;    // PK panels of fmap1 / fmap2 (pack_kernel)
+    const char* pk1;    // f16 hi/lo operand panels of fmap1 / fmap2 (pack_both_kernel)
     const char* pk2;
-    int dev_pk_pipe;
-    int gm;             // m-tiles per group of the grouped tile order    // software-pipelined PK loop (default 1; ECORR_BUILD_PKPIPE=0 for A/B)
     // filled by launch_build
-    int n_mt, n_nt, n_ntx, n_tiles;
+    int n_mt;           // 128-query tiles (fp32 blocks; fmap1 panels)
+    int n_qt;           // 256-query tiles (split blocks)
+    int n_nt, n_ntx;    // n-tiles (target blocks); regular n-tiles per tile row
     int n_reg, band_y0;  // regular (8 x 16) n-tiles per m-tile; first row of the 4-row band tiles
     int fused_levels;   // levels written by the GEMM epilogue (<= 4)
-    int dev_skip_epilogue;  // A/B ablation only (ECORR_BUILD_SKIP_EPILOGUE): 1 no epilogue, 2 no level-0 stores,
-                            // -1 / -4 / -3 no level-2+3 / level-2 / level-3 stores, -5 scalar level-3 stores
     float* lvl[4];
     int lh[4], lw[4];
     int lntx[4], lnty[4];   // tiles per tile row (0 = compact row-major) / tile rows of each fused level
@@ -63,8 +61,6 @@ struct LookupParams {
     int lh[ECORR_MAX_LEVELS], lw[ECORR_MAX_LEVELS];
     int lntx[ECORR_MAX_LEVELS];      // tiles per tile row (0 = compact row-major)
     int lsz[ECORR_MAX_LEVELS];       // floats per query image
-    int dev_skip_mask;               // A/B ablation only (ECORR_LOOKUP_SKIP): levels whose window
-                                     // loads are dropped (output invalid)
 };
 
 int launch_lookup(const LookupParams& P, int B, hipStream_t stream);

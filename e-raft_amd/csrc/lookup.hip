@@ -10,8 +10,6 @@
 // window staging (phases 0-1) is lookup_stage.h; phase 2 writes every output from LDS with lanes
 // = 64 consecutive queries, so each channel store is one 256-byte coalesced row of the NCHW
 // output, stored non-temporally.
-#include <stdlib.h>
-
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
 #include "lookup_stage.h"
@@ -48,73 +46,14 @@ __global__ __launch_bounds__(4 * QB) void lookup_staged(LookupParams P) {
     }
 }
 
-// Same work as lookup_staged with 3 threads per query instead of 4, so that a thread owns whole
-// x-offset columns a in {3p, 3p+1, 3p+2} (K = 2r+1 divisible by 3): the per-query window origin,
-// the 9 row offsets and y weights sit in registers, the x offset and weight load once per column,
+// 3 threads per query instead of lookup_staged's 4, so that a thread owns whole x-offset columns
+// a in {3p, 3p+1, 3p+2} (K = 2r+1 divisible by 3): the x offset and weight load once per column,
 // the per-output work is one address add, two ds_read2 and the 8-op ATen blend, and the output
 // row of channel k is a buffer store whose channel offset is a scalar (k is wave-uniform because
-// a wave is one `part`).  The 4-thread version spent ~35 VALU/LDS instructions and two dependent
-// LDS round trips per output.
-template <int R, int QB>
-__global__ __launch_bounds__(3 * QB) void lookup_cols(LookupParams P) {
-    constexpr int NTQ = 3 * QB, K = 2 * R + 1, AP = K / 3;
-    static_assert(K % 3 == 0 && QB == kWave, "one wave per part, whole columns per part");
-    using WS = WindowStage<R, QB>;
-    constexpr int S = WS::S, SP = WS::SP, KK = WS::KK;
-    __shared__ WS st;
-    const int tid = threadIdx.x, g = tid % QB;
-    const int part = __builtin_amdgcn_readfirstlane(tid / QB);   // wave-uniform
-    const int lv = blockIdx.y, b = blockIdx.z;
-    const int q0 = blockIdx.x * QB;
-    stage_level<R, QB, NTQ>(st, P, lv, b, q0, tid);
-
-    const int md = st.org[g][2] & 0xff;
-    if (md == 2) return;   // past the range (no barrier follows)
-    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-        P.out + (int64_t)b * P.C * P.q_count, 0, P.C * P.q_count * 4, 0x00020000);
-    const int voff = (q0 + g) * 4;
-    const int sbase = lv * KK * P.q_count * 4;
-    if (md == 0) {
-        const int o0 = st.org[g][0], o1 = st.org[g][1];
-        int yo[K];
-        float nb[K];
-#pragma unroll
-        for (int bb = 0; bb < K; ++bb) {
-            yo[bb] = ((int)st.fy[g][bb] - o1) * S;
-            nb[bb] = st.wy[g][bb];
-        }
-        const float* wq = st.win + g * SP;
-#pragma unroll
-        for (int ai = 0; ai < AP; ++ai) {
-            const int a = part * AP + ai;
-            const float* wc = wq + ((int)st.fx[g][a] - o0);
-            const float wa = st.wx[g][a];
-#pragma unroll
-            for (int bb = 0; bb < K; ++bb) {
-                const float* c = wc + yo[bb];
-                const float v = blend(c[0], c[1], c[S], c[S + 1], wa, nb[bb]);
-                // non-temporal (see lookup_staged)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
-                                                      sbase + (a * K + bb) * P.q_count * 4, 2);
-            }
-        }
-    } else {   // coordinates that do not fit the window: exact direct gather
-#pragma unroll 1
-        for (int ai = 0; ai < AP; ++ai)
-#pragma unroll 1
-            for (int bb = 0; bb < K; ++bb) {
-                const int k = (part * AP + ai) * K + bb;
-                const float v = sample_level<R, QB>(st, P, lv, b, q0, g, k, 1);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
-                                                      sbase + k * P.q_count * 4, 2);
-            }
-    }
-}
-
-// lookup_cols with the coordinate chains in registers instead of LDS: every thread computes the
-// 2r+1 y chains and the x chains of its own columns (+ the two x end points for the window
-// check) itself, so the only LDS is the windows and their origins (31.7 KB at r = 4: 5 blocks per
-// CU instead of 4).  Same arithmetic, same bits.
+// a wave is one `part`).  Every thread computes the 2r+1 y chains and the x chains of its own
+// columns (+ the two x end points for the window check) in registers, so the only LDS is the
+// windows and their origins (31.7 KB at r = 4: 5 blocks per CU).  Round-1 A/B: the 4-thread
+// kernel with per-output k decoding 61 vs 48.5 us; chains shared through LDS 2.8% slower.
 template <int R, int QB>
 __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
     constexpr int NTQ = 3 * QB, K = 2 * R + 1, AP = K / 3;
@@ -252,45 +191,26 @@ inline int hip_status() {
 
 }  // namespace
 
-template <int QB>
-static void launch_staged(const LookupParams& P, int B, hipStream_t stream) {
-    const dim3 grid((unsigned)((P.q_count + QB - 1) / QB), (unsigned)P.levels, (unsigned)B);
-    const dim3 block(4 * QB);
-    switch (P.radius) {
-        case 0: hipLaunchKernelGGL((lookup_staged<0, QB>), grid, block, 0, stream, P); break;
-        case 1: hipLaunchKernelGGL((lookup_staged<1, QB>), grid, block, 0, stream, P); break;
-        case 2: hipLaunchKernelGGL((lookup_staged<2, QB>), grid, block, 0, stream, P); break;
-        case 3: hipLaunchKernelGGL((lookup_staged<3, QB>), grid, block, 0, stream, P); break;
-        default: hipLaunchKernelGGL((lookup_staged<4, QB>), grid, block, 0, stream, P); break;
-    }
-}
-
-int launch_lookup(const LookupParams& Pin, int B, hipStream_t stream) {
-    LookupParams P = Pin;
-    const char* ks = getenv("ECORR_LOOKUP_SKIP");   // dev knob (A/B ablation): level bitmask
-    P.dev_skip_mask = ks ? atoi(ks) : 0;
+int launch_lookup(const LookupParams& P, int B, hipStream_t stream) {
     if (P.radius > 4) {
         const int64_t n = (int64_t)B * P.C * P.q_count;
         hipLaunchKernelGGL(lookup_direct, dim3(grid_for(n)), dim3(NT), 0, stream, P, B);
         return hip_status();
     }
-    // dev knobs for A/B timing (tools/ab_lookup.py): ECORR_LOOKUP_QB = 16 | 64 (4-thread kernel),
-    // ECORR_LOOKUP_V=4 forces the 4-thread kernel for radii that have a 3-thread one
-    const char* kq = getenv("ECORR_LOOKUP_QB");
-    const char* kv = getenv("ECORR_LOOKUP_V");
-    const int qb = kq ? atoi(kq) : 64;
-    const bool cols = !kq && !(kv && atoi(kv) == 4) && (P.radius == 4 || P.radius == 1) &&
-                      (int64_t)P.C * P.q_count * 4 < 0x7fffffff;
+    const dim3 grid((unsigned)((P.q_count + 63) / 64), (unsigned)P.levels, (unsigned)B);
+    const bool cols = (P.radius == 4 || P.radius == 1) && (int64_t)P.C * P.q_count * 4 < 0x7fffffff;
     if (cols) {
-        const dim3 grid((unsigned)((P.q_count + 63) / 64), (unsigned)P.levels, (unsigned)B);
-        // ECORR_LOOKUP_V=3 (dev, A/B): the LDS-chain kernel lookup_cols (2.8% slower)
-        if (kv && atoi(kv) == 3) {
-            if (P.radius == 4) hipLaunchKernelGGL((lookup_cols<4, 64>), grid, dim3(192), 0, stream, P);
-            else hipLaunchKernelGGL((lookup_cols<1, 64>), grid, dim3(192), 0, stream, P);
-        } else if (P.radius == 4) hipLaunchKernelGGL((lookup_cols_reg<4, 64>), grid, dim3(192), 0, stream, P);
+        if (P.radius == 4) hipLaunchKernelGGL((lookup_cols_reg<4, 64>), grid, dim3(192), 0, stream, P);
         else hipLaunchKernelGGL((lookup_cols_reg<1, 64>), grid, dim3(192), 0, stream, P);
-    } else if (qb == 16) launch_staged<16>(P, B, stream);
-    else launch_staged<64>(P, B, stream);
+        return hip_status();
+    }
+    switch (P.radius) {
+        case 0: hipLaunchKernelGGL((lookup_staged<0, 64>), grid, dim3(256), 0, stream, P); break;
+        case 1: hipLaunchKernelGGL((lookup_staged<1, 64>), grid, dim3(256), 0, stream, P); break;
+        case 2: hipLaunchKernelGGL((lookup_staged<2, 64>), grid, dim3(256), 0, stream, P); break;
+        case 3: hipLaunchKernelGGL((lookup_staged<3, 64>), grid, dim3(256), 0, stream, P); break;
+        default: hipLaunchKernelGGL((lookup_staged<4, 64>), grid, dim3(256), 0, stream, P); break;
+    }
     return hip_status();
 }
 

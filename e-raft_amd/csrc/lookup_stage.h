@@ -146,8 +146,7 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const Lookup
         const int x = st.org[gq][0] + rx, y0 = st.org[gq][1], info = st.org[gq][2];
         const int ny = (info >> 16) & 0xff;
         // only the needed corner rectangle touches memory; the slack row/column reads 0 for free
-        const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) && (unsigned)x < (unsigned)w &&
-                           !((P.dev_skip_mask >> lv) & 1);
+        const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) && (unsigned)x < (unsigned)w;
         dst[c] = live ? gq * SP + rx : -1;
         // rows ry in [rlo, rhi) are needed and inside the image; the column's byte offset walks
         // down the rows incrementally (tiled: +8 floats inside a tile, + one tile row minus 24 from

@@ -22,7 +22,6 @@
 // Numerics: the samples are bit-exact; the channel sum is an exact c-ordered fmaf chain (fp32
 // MFMA), then + bias, then ReLU (torch.relu semantics: NaN stays NaN) -- normwise agreement with
 // the reference's conv (its reduction order belongs to MKL/MIOpen).
-#include <stdlib.h>
 
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
@@ -44,7 +43,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 template <int R>
 __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, const float* __restrict__ wt /* [O][C] */,
                                                              const float* __restrict__ bias, int O,
-                                                             float* __restrict__ out, int dev_phase) {
+                                                             float* __restrict__ out) {
     using WS = WindowStage<R, QBM>;
     constexpr int KK = WS::KK;
     constexpr int CPAD = ((4 * KK + KC - 1) / KC) * KC;   // levels <= 4; rows padded to whole chunks
@@ -64,7 +63,7 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
     const int C = P.C;
 
     // ---- lookup: the block's corr tile, level by level, into T (rows >= C zero)
-    for (int lv = 0; lv < (dev_phase == 2 ? 0 : P.levels); ++lv) {
+    for (int lv = 0; lv < P.levels; ++lv) {
         stage_level<R, QBM, NTM>(u.st, P, lv, b, q0, tid);
         const int md = u.st.org[g][2] & 0xff;
         if (md == 0) {   // staged window: origin hoisted, no mode test per sample
@@ -91,11 +90,6 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
         __syncthreads();   // the stage is rebuilt by the next level / reused by the weight chunks
     }
     for (int i = C * QBM + tid; i < CPAD * QBM; i += NTM) T[i / QBM][i % QBM] = 0.0f;
-    if (dev_phase == 1) {   // A/B timing only: lookup phase alone
-        __syncthreads();
-        if (tid < QBM && q0 + tid < P.q_count) out[(int64_t)b * O * P.q_count + q0 + tid] = T[tid % C][tid];
-        return;
-    }
 
     // ---- GEMM over the channels, no barrier inside: each lane streams its own weight row
     // W[o][c] (o = ob + lane&31, + 32 for the second tile) straight from L2 in float4 pieces, one
@@ -167,13 +161,11 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
 
 int launch_lookup_conv(const LookupParams& P, int B, const float* wt, const float* bias, int O, float* out,
                        hipStream_t stream) {
-    if (P.radius != 4 || P.levels > 4) return ECORR_ERADIUS;
+    if (P.radius != 4) return ECORR_ERADIUS;
+    if (P.levels > 4) return ECORR_ELEVELS;
     if (O <= 0 || O % OW != 0) return ECORR_EINVAL;
     const dim3 grid((unsigned)((P.q_count + QBM - 1) / QBM), (unsigned)B), block(NTM);
-    // dev knob for A/B timing (tools/ab_motion.py): ECORR_FUSED_PHASE=1 lookup only, 2 GEMM only
-    const char* kp = getenv("ECORR_FUSED_PHASE");
-    const int phase = kp ? atoi(kp) : 0;
-    hipLaunchKernelGGL(lookup_conv_kernel<4>, grid, block, 0, stream, P, wt, bias, O, out, phase);
+    hipLaunchKernelGGL(lookup_conv_kernel<4>, grid, block, 0, stream, P, wt, bias, O, out);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
 }

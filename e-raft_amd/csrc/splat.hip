@@ -18,7 +18,6 @@
 // points at 1280x720), so the counts live in LDS (<= 16384 targets) and the work is latency-bound
 // (a few microseconds), not bandwidth-bound: in LDS mode (DSEC, MVSEC) all four phases run out of
 // LDS; larger maps keep keys (and counts past 16384 targets) in the caller's workspace.
-#include <stdlib.h>
 
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
@@ -40,7 +39,6 @@ struct SplatArgs {
     int* ws_keys;       // [B][4n] (global mode)
     int64_t n;
     int h, w;
-    int dev_stop;       // A/B timing only (ECORR_SPLAT_STOP=k): return after phase k
 };
 
 // Floats per point: FLOW -> (dx, dy); points -> (x, y, z).
@@ -110,7 +108,6 @@ __global__ __launch_bounds__(NTS) void splat_kernel(SplatArgs A) {
 
     for (int t = tid; t < hw; t += NTS) cnt[t] = 0;
     __syncthreads();
-    if (A.dev_stop == 0) return;
 
     // 1. count
     for (int s = tid; s < n; s += NTS) {
@@ -123,7 +120,6 @@ __global__ __launch_bounds__(NTS) void splat_kernel(SplatArgs A) {
         }
     }
     __syncthreads();
-    if (A.dev_stop == 1) return;
 
     // 2. exclusive scan; each thread owns SPT consecutive counts of a super-chunk
     constexpr int SPT = 8;
@@ -157,7 +153,6 @@ __global__ __launch_bounds__(NTS) void splat_kernel(SplatArgs A) {
         if (tid == NTS - 1) carry_s = run;
     }
     __syncthreads();
-    if (A.dev_stop == 2) return;
 
     // 3. fill buckets (cnt[t] walks from the bucket start to the next bucket's start) in rounds
     // of NTS consecutive points of one pass, a barrier between rounds: slots are handed out in
@@ -174,7 +169,6 @@ __global__ __launch_bounds__(NTS) void splat_kernel(SplatArgs A) {
             }
             __syncthreads();
         }
-    if (A.dev_stop == 3) return;
 
     // 4. per target: order the bucket, fold in key order from +0 (put_ into torch.zeros)
     float* vout = A.values + (int64_t)b * NZ * hw;
@@ -234,8 +228,6 @@ int launch_splat(bool flow_mode, const float* pts, int B, int64_t n, int h, int 
     A.h = h;
     A.w = w;
     const int64_t hw = (int64_t)h * w;
-    const char* ks = getenv("ECORR_SPLAT_STOP");
-    A.dev_stop = ks ? atoi(ks) : 99;
     int* ws = (int*)workspace;
     A.ws_count = hw > kLdsTargets ? ws : nullptr;
     A.ws_keys = ws ? ws + (hw > kLdsTargets ? (int64_t)B * hw : 0) : nullptr;

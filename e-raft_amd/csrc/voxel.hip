@@ -11,7 +11,8 @@
 //           pass-0 corner lands in; DSEC keys live on a grid extended by one cell on the low side
 //           because x0 = -1 still reaches x = 0) and the per-event factors the weights need;
 //   bucket  counting sort by key: per-key counts (integer atomics, in prep), exclusive scan
-//           (rocPRIM), events dropped into their key's run (integer atomics pick the slot);
+//           (reduce -> scan of the tile sums -> tile scans), events dropped into their key's run
+//           (integer atomics pick the slot);
 //   order   per key, its run insertion-sorted by event index (runs are short and the atomics
 //           hand out slots nearly in event order, so this is ~linear) and the events' weight
 //           factors gathered once into run order (one float4 each);
@@ -25,9 +26,6 @@
 //           values agree within an ulp or two.
 // Memory-bound with random event access; every phase is a full-chip launch.
 #include <algorithm>
-#include <cstring>   // rocprim's texture_cache_iterator uses memset without including it
-
-#include <rocprim/device/device_scan.hpp>
 
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
@@ -243,23 +241,84 @@ __global__ __launch_bounds__(NTV) void norm_apply(float* __restrict__ g, int64_t
     }
 }
 
+// Exclusive uint32 scan of the per-key counts (wrapping adds, like any uint32 scan): SCAN_T
+// elements per block tile; phase 1 writes each tile's sum, phase 2 (one block) scans the sums,
+// phase 3 scans each tile from its offset.  Integer arithmetic: exact in any order.
+constexpr int SCAN_PER = 16, SCAN_T = NTV * SCAN_PER;
+
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int w = 0; w < wv; ++w) pre += sh[w];
+    total = sh[0] + sh[1] + sh[2] + sh[3];
+    __syncthreads();
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(NTV) void scan_reduce(const uint32_t* __restrict__ in, uint32_t K, uint32_t* __restrict__ sums) {
+    __shared__ uint32_t sh[NTV / 64];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_T + threadIdx.x * SCAN_PER;
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k)
+        if (base + k < K) v += in[base + k];
+    uint32_t total;
+    block_exclusive_scan(v, sh, total);
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(NTV) void scan_sums(uint32_t* __restrict__ sums, int nb) {
+    __shared__ uint32_t sh[NTV / 64];
+    uint32_t carry = 0;
+    for (int c = 0; c < nb; c += NTV) {
+        const int i = c + threadIdx.x;
+        const uint32_t v = i < nb ? sums[i] : 0;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan(v, sh, total);
+        if (i < nb) sums[i] = carry + ex;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(NTV) void scan_apply(const uint32_t* __restrict__ in, uint32_t K, const uint32_t* __restrict__ sums,
+                                                  uint32_t* __restrict__ out) {
+    __shared__ uint32_t sh[NTV / 64];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_T + threadIdx.x * SCAN_PER;
+    uint32_t v[SCAN_PER], s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {
+        v[k] = base + k < K ? in[base + k] : 0;
+        s += v[k];
+    }
+    uint32_t total;
+    uint32_t run = sums[blockIdx.x] + block_exclusive_scan(s, sh, total);
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {
+        if (base + k < K) out[base + k] = run;
+        run += v[k];
+    }
+}
+
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + NTV - 1) / NTV); }
 
 inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // Workspace carve-up (every piece 256-byte aligned).
 struct VoxelWs {
-    size_t key, cnt, off, slot, fa, fb, payload, norm, part, scan_tmp, total;
-    size_t scan_bytes;
+    size_t key, cnt, off, slot, fa, fb, payload, norm, part, scan_sums, total;
 };
 
 constexpr int kGatherBlocks = 2048;   // grid-stride gather: this many normalization partials
 
 int plan(int64_t n, uint32_t K, int64_t cells, VoxelWs* w) {
-    size_t scan_bytes = 0;
-    const hipError_t e = rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
-                                                 (size_t)K, rocprim::plus<uint32_t>());
-    if (e != hipSuccess) return ECORR_EHIP - (int)e;
     (void)cells;
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t at = o; o += align256(bytes); return at; };
@@ -272,8 +331,7 @@ int plan(int64_t n, uint32_t K, int64_t cells, VoxelWs* w) {
     w->payload = take(16 * (size_t)n);
     w->norm = take(sizeof(NormState));
     w->part = take(3 * 8 * (size_t)kGatherBlocks);
-    w->scan_bytes = scan_bytes;
-    w->scan_tmp = take(scan_bytes);
+    w->scan_sums = take(4 * (((size_t)K + SCAN_T - 1) / SCAN_T));
     w->total = o;
     return ECORR_OK;
 }
@@ -325,10 +383,14 @@ int launch_voxel(bool dsec, const float* p, const float* t, const float* x, cons
     if (dsec) hipLaunchKernelGGL(prep_dsec, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
     else hipLaunchKernelGGL(prep_mvsec, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
     if ((st = hip_status()) != ECORR_OK) return st;
-    size_t scan_bytes = w.scan_bytes;
-    e = rocprim::exclusive_scan(base + w.scan_tmp, scan_bytes, A.cnt, A.off, 0u, (size_t)A.K,
-                                rocprim::plus<uint32_t>(), stream);
-    if (e != hipSuccess) return ECORR_EHIP - (int)e;
+    {
+        const unsigned nb = (unsigned)(((size_t)A.K + SCAN_T - 1) / SCAN_T);
+        uint32_t* sums = (uint32_t*)(base + w.scan_sums);
+        hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(NTV), 0, stream, A.cnt, A.K, sums);
+        hipLaunchKernelGGL(scan_sums, dim3(1), dim3(NTV), 0, stream, sums, (int)nb);
+        hipLaunchKernelGGL(scan_apply, dim3(nb), dim3(NTV), 0, stream, A.cnt, A.K, sums, A.off);
+        if ((st = hip_status()) != ECORR_OK) return st;
+    }
     hipLaunchKernelGGL(fill_runs, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
     if (dsec) hipLaunchKernelGGL(order_runs<true>, dim3(blocks_for(A.K)), dim3(NTV), 0, stream, A);
     else hipLaunchKernelGGL(order_runs<false>, dim3(blocks_for(A.K)), dim3(NTV), 0, stream, A);

@@ -89,7 +89,8 @@ int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W,
  * out float[B][O][q_count] = relu(bias[o] + sum_c weight[o][c] * corr[b][c][p]), where corr is
  * exactly what ecorr_lookup would return (C = levels*(2r+1)^2 channels) and never leaves the chip.
  * weight: float[O][C] (the conv weight [O][C][1][1] as stored), bias: float[O] or NULL.
- * radius must be 4 and levels <= 4 (else ECORR_ERADIUS), O a positive multiple of 64.
+ * radius must be 4 (else ECORR_ERADIUS), levels <= 4 (else ECORR_ELEVELS), O a positive multiple
+ * of 64 (else ECORR_EINVAL).
  * Replaces: CorrBlock.__call__ (corr.py:29-50) + F.relu(self.convc1(corr)) (update.py:67,74). */
 int ecorr_lookup_conv1x1_relu(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
                               int levels, int radius, const float* weight, const float* bias, int O,

@@ -40,6 +40,16 @@ def test_header_symbols_exported(ea):
     assert exported == set(names)
 
 
+def test_library_reads_no_environment(ea):
+    """No runtime knobs: the library imports no getenv/secure_getenv, so a stray variable cannot
+    change a result (round 1 read ECORR_BUILD_SKIP_EPILOGUE & co. on every launch)."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", ea.LIB_PATH], capture_output=True, text=True).stdout
+    assert not re.search(r"\bU (secure_)?getenv\b", out), out
+    for src in sorted(os.listdir(os.path.join(ROOT, "e-raft_amd", "csrc"))):
+        if src.endswith((".hip", ".h")):
+            assert "getenv" not in open(os.path.join(ROOT, "e-raft_amd", "csrc", src)).read(), src
+
+
 def test_code_object_is_gfx950(ea):
     # the embedded HIP fat binary names its offload targets (amdgcn-amd-amdhsa--gfx950)
     data = open(ea.LIB_PATH, "rb").read()
@@ -90,7 +100,7 @@ def test_argument_validation_before_launch(ea):
     # fused lookup + convc1: radius 4 / <= 4 levels only, O a multiple of 64, weight required
     F = L.ecorr_lookup_conv1x1_relu
     assert F(8, 8, 1, 16, 16, 256, 4, 3, 8, None, 64, 8, None) == _lib.ECORR_ERADIUS
-    assert F(8, 8, 1, 64, 64, 4096, 5, 4, 8, None, 64, 8, None) == _lib.ECORR_ERADIUS
+    assert F(8, 8, 1, 64, 64, 4096, 5, 4, 8, None, 64, 8, None) == _lib.ECORR_ELEVELS   # levels > 4
     assert F(8, 8, 1, 16, 16, 256, 4, 4, 8, None, 96, 8, None) == _lib.ECORR_EINVAL
     assert F(8, 8, 1, 16, 16, 256, 4, 4, None, None, 64, 8, None) == _lib.ECORR_EINVAL
 

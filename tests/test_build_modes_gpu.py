@@ -99,42 +99,97 @@ def test_split_query_slab_matches_whole(ea):
 
 
 
-@pytest.mark.parametrize("case", [(2, 256, 16, 24, 1.0, 7), (1, 100, 17, 22, 1e-3, 8)],
-                         ids=lambda c: "b%d_d%d_%dx%d_s%g" % c[:5])
-def test_split_inloop_fallback(ea, case, monkeypatch):
-    """The split build's fallback (panels too large for one buffer range: the operands split in
-    the K loop instead of by pack_kernel; forced here with ECORR_BUILD_PK=0, read per launch)
-    meets the same bar on the vector and the ragged (register-staged) loops."""
-    B, D, H, W, scale, seed = case
-    f1n = (prng.normal(10 * seed, (B, D, H, W)) * np.float32(scale)).astype(np.float32)
-    f2n = (prng.normal(10 * seed + 1, (B, D, H, W)) * np.float32(scale)).astype(np.float32)
+def _heavy_cases():
+    """Operands at the split's documented precision limit (build.hip: lo keeps 11 bits down to
+    2^-17 of a pixel's maximum, f16 subnormals below): per-pixel dynamic range 2^17 and 2^24,
+    ReLU-sparse channels (half and 90% exact zeros), log-normal heavy tails, one dominant channel."""
+    B, D, H, W = 2, 256, 24, 32
+    out = []
+    for k, (name, gen) in enumerate([
+            ("range2^17", lambda s: prng.normal(s, (B, D, H, W)) * np.exp2(-17.0 * prng.uniform(s + 7, (B, D, H, W), 0, 1))),
+            ("range2^24", lambda s: prng.normal(s, (B, D, H, W)) * np.exp2(-24.0 * prng.uniform(s + 7, (B, D, H, W), 0, 1))),
+            ("relu50", lambda s: np.maximum(prng.normal(s, (B, D, H, W)), 0)),
+            ("relu90", lambda s: np.maximum(prng.normal(s, (B, D, H, W)) - 1.2816, 0)),
+            ("lognormal", lambda s: prng.normal(s, (B, D, H, W)) * np.exp(2.0 * prng.normal(s + 7, (B, D, H, W)))),
+            ("dominant", lambda s: prng.normal(s, (B, D, H, W)) * np.where(np.arange(D)[None, :, None, None] == 3, 1e5, 1.0)),
+    ]):
+        out.append((name, gen(100 + 10 * k).astype(np.float32), gen(101 + 10 * k).astype(np.float32)))
+    return out
+
+
+@pytest.mark.parametrize("case", _heavy_cases(), ids=lambda c: c[0])
+def test_split_precision_limits(ea, case):
+    """Normwise <= 1e-5 vs fp64 and no worse than the fp32-MFMA GEMM where features have a wide
+    within-pixel dynamic range, exact zeros or heavy tails."""
+    name, f1n, f2n = case
     f1, f2 = torch.from_numpy(f1n).to(DEV), torch.from_numpy(f2n).to(DEV)
     truth = oracle.corr_level0(f1n, f2n)
-    monkeypatch.setenv("ECORR_BUILD_PK", "0")
+    errs = {}
     with torch.no_grad():
-        lv = _build(ea, f1, f2, "split", levels=3)
-    err = oracle.normwise_err(lv[0], truth)
-    print(f"in-loop split normwise vs fp64 {err:.2e}")
-    assert err <= GEMM_TOL
-    ref_levels = oracle.pyramid_from_level0(lv[0], 3)
-    for i in range(1, 3):
-        assert oracle.same_bits(lv[i], ref_levels[i]), f"level {i}"
+        for mode in ("fp32", "split"):
+            lv = _build(ea, f1, f2, mode, levels=3)
+            errs[mode] = oracle.normwise_err(lv[0], truth)
+    print(f"{name}: normwise vs fp64 fp32 {errs['fp32']:.2e} split {errs['split']:.2e}")
+    if name != "lognormal":
+        assert errs["fp32"] <= GEMM_TOL and errs["split"] <= GEMM_TOL
+    # log-normal tails (e^{2 N(0,1)} scales) make the products cancel: sum |a_k b_k| is far above
+    # |sum a_k b_k|, so no fp32-accumulating GEMM meets 1e-5 normwise vs fp64 there (the fp32-MFMA
+    # chain measures 3.3e-5; the reference's sgemm accumulates in fp32 too).  The bar for that
+    # case is the reference-faithful one: no worse than the fp32 GEMM.  Where ONE product dominates
+    # each dot product ("dominant", a channel 1e5 x the rest) nothing averages out and the split's
+    # per-product error (2^-22 relative: lo*lo is dropped) exceeds the fp32 chain's (one rounding,
+    # 2^-24): 1.6e-6 vs 4e-7 measured, still 6x under the bar; hence the 2e-6 floor.
+    assert errs["split"] <= max(errs["fp32"], 2e-6)
 
 
-@pytest.mark.parametrize("case", [(2, 256, 16, 24, 1.0, 9), (3, 100, 17, 22, 1e-3, 10), (1, 256, 60, 80, 1.0, 11),
-                                  (2, 64, 5, 300, 3e4, 12)],
-                         ids=lambda c: "b%d_d%d_%dx%d_s%g" % c[:5])
-def test_split_single_pack_launch_matches_two(ea, case, monkeypatch):
-    """Both operand passes run as ONE launch (pack_both_kernel, grid z = operand, surplus x blocks
-    of the shorter pass return at once).  Shapes with n_mt != n_nt (ragged 17x22, the band tiles of
-    a 5-row map, DSEC 60x80) must give the pyramid bit for bit as one launch per operand
-    (ECORR_BUILD_PACK2=1, read per launch)."""
-    B, D, H, W, scale, seed = case
-    f1 = torch.from_numpy((prng.normal(10 * seed, (B, D, H, W)) * np.float32(scale)).astype(np.float32)).to(DEV)
-    f2 = torch.from_numpy((prng.normal(10 * seed + 1, (B, D, H, W)) * np.float32(scale)).astype(np.float32)).to(DEV)
+def test_split_precision_real_fnet_features(ea):
+    """The same bar on real feature maps: E-RAFT's fnet (PRNG weights at the reference's init
+    scales, tests/e2e_weights.py) applied to PRNG event volumes, 256 x 320 input -> 32 x 40."""
+    import eraft_amd.network as nw
+    from e2e_weights import make_state_dict
+    net = nw.ERAFT({"subtype": "standard"}, n_first_channels=15)
+    net.load_state_dict(make_state_dict(net.state_dict()))
+    net = net.eval().to(DEV)
+    im1 = torch.from_numpy(prng.normal(41, (1, 15, 256, 320))).to(DEV)
+    im2 = torch.from_numpy(prng.normal(42, (1, 15, 256, 320))).to(DEV)
     with torch.no_grad():
-        one = _build(ea, f1, f2, "split", levels=3)
-        monkeypatch.setenv("ECORR_BUILD_PACK2", "1")
-        two = _build(ea, f1, f2, "split", levels=3)
-    for i in range(3):
-        assert oracle.same_bits(one[i], two[i]), f"level {i}"
+        f1, f2 = net.fnet([im1, im2])
+        f1, f2 = f1.float().contiguous(), f2.float().contiguous()
+        assert f1.shape == (1, 256, 32, 40)
+        f1n, f2n = f1.cpu().numpy(), f2.cpu().numpy()
+        truth = oracle.corr_level0(f1n, f2n)
+        errs = {m: oracle.normwise_err(_build(ea, f1, f2, m)[0], truth) for m in ("fp32", "split")}
+    frac0 = float((f1n == 0).mean())
+    print(f"fnet features (zeros {frac0:.1%}): fp32 {errs['fp32']:.2e} split {errs['split']:.2e}")
+    assert errs["fp32"] <= GEMM_TOL and errs["split"] <= GEMM_TOL
+    assert errs["split"] <= max(errs["fp32"], 1e-6)
+
+
+def test_stray_dev_env_vars_change_nothing(ea, monkeypatch):
+    """Round 1 read A/B knobs with getenv on every launch (ECORR_BUILD_SKIP_EPILOGUE dropped pyramid
+    stores with status ECORR_OK).  The library reads no environment: setting every old knob must
+    leave the pyramid, the lookup and the fused lookup bit for bit unchanged."""
+    import eraft_amd
+    B, D, H, W = 2, 256, 23, 40
+    f1 = torch.from_numpy(prng.normal(61, (B, D, H, W))).to(DEV)
+    f2 = torch.from_numpy(prng.normal(62, (B, D, H, W))).to(DEV)
+    coords = torch.from_numpy(prng.coords_with_flow(63, B, H, W, 3.0)).to(DEV)
+    wt = torch.from_numpy(prng.normal(64, (256, 324)) * np.float32(0.05)).to(DEV)
+
+    def run():
+        with torch.no_grad():
+            blk = eraft_amd.CorrBlock(f1, f2)
+            outs = [lv.clone() for lv in blk.corr_pyramid] + [blk(coords), blk.lookup_conv1x1_relu(coords, wt)]
+            torch.cuda.synchronize()
+        return outs
+
+    clean = run()
+    for k, v in {"ECORR_BUILD_SKIP_EPILOGUE": "1", "ECORR_BUILD_PK": "0", "ECORR_BUILD_PACK2": "1",
+                 "ECORR_BUILD_ABL": "5", "ECORR_BUILD_GM": "2", "ECORR_BUILD_KB32": "1", "ECORR_BUILD_GLDS": "0",
+                 "ECORR_BUILD_NOBAND": "1", "ECORR_BUILD_PKPIPE": "0", "ECORR_LOOKUP_SKIP": "15",
+                 "ECORR_LOOKUP_QB": "16", "ECORR_LOOKUP_V": "4", "ECORR_FUSED_PHASE": "1",
+                 "ECORR_SPLAT_STOP": "0"}.items():
+        monkeypatch.setenv(k, v)
+    dirty = run()
+    for a, b in zip(clean, dirty):
+        assert torch.equal(a, b)

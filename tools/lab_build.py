@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Lab builds of libecorr.so for A/B and ablation (dev tool; the product has no runtime knobs).
+
+Copies e-raft_amd/csrc + include to tools/<name>_lab/, applies the named source patches (exact
+string replacements, each must match) and builds tools/<name>_lab/e-raft_amd/libecorr.so, which
+tools/ab_build.py loads as AB_ALT_LIB.  Ablation variants produce invalid pyramids (AB_NOCHECK=1).
+  python tools/lab_build.py noepi nomfma ...
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EPI = "    // ---------------- epilogue (per wave, from registers) ----------------\n"
+
+# name -> list of (file, old, new)
+PATCHES = {
+    # epilogue replaced by one store per lane of the accumulator sum
+    "noepi": [("build.hip", EPI, EPI + """    {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s += acc[i][j][r];
+        P.lvl[0][(int64_t)blockIdx.x * 256 + tid] = s;
+        return;
+    }
+""")],
+    # K loop without its MFMAs (fragments kept alive)
+    "nomfma": [("build.hip", "                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.th[j], f.ql[i], acc[i][j], 0, 0, 0);",
+                "                asm volatile(\"\" :: \"v\"(f.th[j]), \"v\"(f.ql[i]));"),
+               ("build.hip", "                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.tl[j], f.qh[i], acc[i][j], 0, 0, 0);",
+                "                asm volatile(\"\" :: \"v\"(f.tl[j]), \"v\"(f.qh[i]));"),
+               ("build.hip", "                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.th[j], f.qh[i], acc[i][j], 0, 0, 0);",
+                "                asm volatile(\"\" :: \"v\"(f.th[j]), \"v\"(f.qh[i]));")],
+    # store cache policy of the level-0/1 segments: sc1, plain (tree: nt sc1)
+    "stsc1": [("build.hip", "constexpr int ST_SC1 = 18;", "constexpr int ST_SC1 = 16;")],
+    "stplain": [("build.hip", "constexpr int ST_SC1 = 18;", "constexpr int ST_SC1 = 0;")],
+    # the second wave of resident blocks starts ~12 us late (do co-resident blocks run in phase?)
+    "stagger": [("build.hip", "    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n    const int acol",
+                 "    if (blockIdx.x >= 256 && blockIdx.x < 512)\n        for (int z = 0; z < 3; ++z) __builtin_amdgcn_s_sleep(127);\n"
+                 "    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n    const int acol")],
+}
+# stores spread over the K loop (4 store instructions per chunk, level-0-line shaped, junk
+# values), epilogue dropped: does spreading the store stream let it overlap the matrix work?
+SPREAD_SLOT = """
+    auto spread_slot = [&](int kc) {
+        const int64_t rows0s = (int64_t)b * P.q_count + q0;
+        const int nqs = min(SQ, P.q_count - q0);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P.lvl[0] + rows0s * P.lsz[0], 0, (int)(nqs * P.lsz[0] * 4), 0x00020000);
+        const int ii = (kc >> 2) & 1, jj = kc & 3, ql = wave * 64 + 32 * ii;
+        const int tr = (tc.ty0 >> 2) + (jj & 1), tcl = (tc.tx0 >> 3) + (jj >> 1);
+        const int base = (int)((ql + 4 * ((lane & 31) >> 2)) * P.lsz[0] * 4) + ((tr * P.lntx[0] + tcl) * kTile) * 4 + 64 * (lane >> 5) + 16 * (lane & 3);
+        const bool ok = kc < 8 && tr < P.lnty[0] && tcl < P.lntx[0];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, floatx4{acc[0][0][s], acc[0][1][s], acc[1][0][s], acc[1][1][s]}), rs,
+                                                   ok ? base + (int)(s * P.lsz[0] * 4) : SOOB, 0, ST_SC1);
+    };
+"""
+PATCHES["spread"] = PATCHES["noepi"] + [
+    ("build.hip", "    Frags fa, fb;\n", SPREAD_SLOT + "    Frags fa, fb;\n"),
+    ("build.hip", "        wait_vm<SCOPIES, true>();", "        wait_vm<SCOPIES + 8, true>();"),
+    ("build.hip", "        advance(kc + 1);\n        read_lo(kc + 1, fb);", "        advance(kc + 1);\n        spread_slot(kc);\n        read_lo(kc + 1, fb);"),
+    ("build.hip", "        advance(kc + 2);\n        read_lo(kc + 2, fa);", "        advance(kc + 2);\n        spread_slot(kc + 1);\n        read_lo(kc + 2, fa);"),
+]
+PATCHES["burst"] = PATCHES["noepi"] + [
+    ("build.hip", "    Frags fa, fb;\n", SPREAD_SLOT + "    Frags fa, fb;\n"),
+    ("build.hip", EPI, "#pragma unroll\n    for (int z = 0; z < 8; ++z) spread_slot(z);\n" + EPI),
+]
+# epilogue pieces: level 0 only (scaling + LDS line transposes + stores); no level-2/3 pixel stores
+PATCHES["l0only"] = [("build.hip", "    const int L = P.fused_levels;\n    const int64_t rows0", "    const int L = 1;\n    const int64_t rows0")]
+PATCHES["nol23"] = [("build.hip", "        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, in ? off : SOOB, 0, 0);",
+                     "        asm volatile(\"\" :: \"v\"(val), \"v\"(in ? off : SOOB));")]
+# per-block timestamps: [start, K loop done, epilogue done] (s_memrealtime, 100 MHz) + HW_ID + XCC_ID,
+# read back with ecorr_lab_stamps(host_ptr, n) (tools/stamps.py)
+STAMP_DECL = """
+__device__ unsigned long long g_stamps[65536][5];
+__device__ __forceinline__ void stamp(int k) {
+    if (threadIdx.x == 0 && blockIdx.x < 65536) {
+        g_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();
+        if (k == 0) g_stamps[blockIdx.x][4] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) << 32) |
+                                             (unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+    }
+}
+"""
+STAMP_EXPORT = """
+extern "C" __attribute__((visibility("default"))) int ecorr_lab_stamps(void* dst, int n) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ecorr::g_stamps), (size_t)n * 40, 0, hipMemcpyDeviceToHost);
+}
+"""
+PATCHES["stamps"] = [
+    ("build.hip", "constexpr int SQ = 256; ", STAMP_DECL + "constexpr int SQ = 256; "),
+    ("build.hip", "    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n    const int acol", "    stamp(0);\n    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n    const int acol"),
+    ("build.hip", "    __builtin_amdgcn_s_barrier();   // ... in every wave: the chunk buffers are the epilogue's scratch\n",
+     "    __builtin_amdgcn_s_barrier();   // ... in every wave: the chunk buffers are the epilogue's scratch\n    stamp(1);\n"),
+    ("build.hip", "                    r1t < P.lnty[1] && c1t < P.lntx[1]);\n    }\n}\n",
+     "                    r1t < P.lnty[1] && c1t < P.lntx[1]);\n    }\n    __builtin_amdgcn_s_barrier();\n    stamp(3);\n    __syncthreads();\n    stamp(2);\n}\n"),
+    ("build.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + STAMP_EXPORT),
+]
+# inside the K loop (wave 0 lane 0 and wave 3): cycles spent in the DMA wait, in the barrier, and
+# in total, summed over the chunks (s_memtime) -> g_stamps[block] = {wait, barrier, total, wave-3 wait}
+PATCHES["loopstamps"] = [
+    ("build.hip", "constexpr int SQ = 256; ", STAMP_DECL + "__device__ unsigned long long g_lw, g_lb;\nconstexpr int SQ = 256; "),
+    ("build.hip", """    auto advance = [&](int j) {
+        wait_vm<SCOPIES, true>();
+        __builtin_amdgcn_s_barrier();""", """    auto advance = [&](int j) {
+        const unsigned long long ta = __builtin_amdgcn_s_memtime();
+        wait_vm<SCOPIES, true>();
+        const unsigned long long tb = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_barrier();
+        const unsigned long long tcb = __builtin_amdgcn_s_memtime();
+        sw += tb - ta; sb += tcb - tb;"""),
+    ("build.hip", "    Frags fa, fb;\n    issue(0);", "    const unsigned long long tl0 = __builtin_amdgcn_s_memtime(), tr0 = __builtin_amdgcn_s_memrealtime();\n    Frags fa, fb;\n    issue(0);"),
+    ("build.hip", "    // chunk j's copies landed (the chunk after it may fly)", "    unsigned long long sw = 0, sb = 0;\n    // chunk j's copies landed (the chunk after it may fly)"),
+    ("build.hip", "    wait_vm<0, true>();             // the trailing zero chunks have landed and this wave's reads are done ...\n",
+     "    wait_vm<0, true>();             // the trailing zero chunks have landed and this wave's reads are done ...\n"
+     "    if (lane == 0 && blockIdx.x < 65536) { if (wave == 0) { g_stamps[blockIdx.x][0] = sw; g_stamps[blockIdx.x][1] = sb; "
+     "g_stamps[blockIdx.x][2] = __builtin_amdgcn_s_memtime() - tl0; } g_stamps[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime() - tr0; }\n"),
+    ("build.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + STAMP_EXPORT),
+]
+COMBOS = {}
+
+
+def build(name):
+    dst = os.path.join(ROOT, "tools", f"{name}_lab")
+    if os.path.exists(dst):
+        shutil.rmtree(dst)
+    shutil.copytree(os.path.join(ROOT, "e-raft_amd", "csrc"), os.path.join(dst, "e-raft_amd", "csrc"),
+                    ignore=shutil.ignore_patterns("build"))
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(dst, "include"))
+    for fname, old, new in [x for n in COMBOS.get(name, [name]) for x in PATCHES[n]]:
+        p = os.path.join(dst, "e-raft_amd", "csrc", fname)
+        s = open(p).read()
+        if old not in s:
+            raise SystemExit(f"{name}: patch target not found in {fname}: {old[:60]!r}")
+        s = s.replace(old, new)
+        open(p, "w").write(s)
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(dst, "e-raft_amd", "csrc")], check=True)
+    print(f"built tools/{name}_lab/e-raft_amd/libecorr.so")
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:]:
+        build(n)

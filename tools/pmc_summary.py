@@ -38,7 +38,7 @@ for k, d in sorted(agg.items()):
     avg = {c: sum(v) / len(v) for c, v in d.items()}
     for c, v in sorted(avg.items()):
         lines.append(f"  {c:28s} {v:16.1f}   (n={len(d[c])})")
-    wide = k.startswith("build_kernel")
+    wide = k.startswith(("build_kernel", "build_split_kernel"))
     rec = {"counters": avg}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         rd = avg["FETCH_SIZE"] * 1024 * (2 if wide else 1)
