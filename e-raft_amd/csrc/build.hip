@@ -139,6 +139,7 @@ constexpr int SCOPIES = SCHUNK / 1024 / 4;  // LDS-DMA copies per wave per chunk
 constexpr int SOOB = 0x7ffffff0;            // buffer offset beyond any panel: loads 0, touches nothing
 constexpr int ST_SC1 = 18;                  // level-0/1 store cache policy: nt sc1 (write through, drop from L2)
 constexpr int XS = 144;                     // LDS bytes per query of the epilogue's line transpose
+static_assert(4 * 4 * 32 * XS <= SNBUF * SCHUNK, "epilogue transpose regions fit the chunk buffers");
 
 // target (y, x) of position p of a split fmap2 panel, relative to the n-tile origin
 __host__ __device__ __forceinline__ void split_target(int p, bool band, int& y, int& x) {
@@ -311,7 +312,9 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
     // (32 queries x 144 B: conflict-free ds_write_b128 and ds_read_b128), then reads back piece m
     // of segment arow of query 4k + s, so the 4 lanes of a quad store 64 contiguous bytes and
     // lanes acol, acol + 32 the two halves of one line.
-    char* xp = smem + wave * (32 * XS);
+    // four regions per wave (one per level-0 line of a tile row; the level-1 line reuses region
+    // 0): no line waits for the previous line's read-back before writing
+    char* const xw = smem + wave * (4 * 32 * XS);
     const int m4 = lane & 3, k4 = acol >> 2;
     const int wo = acol * XS, ro = (4 * k4) * XS + 64 * arow + 16 * m4;
     const int L = P.fused_levels;
@@ -322,7 +325,7 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
         return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + rows0 * P.lsz[lv], 0, (int)(nq * P.lsz[lv] * 4), 0x00020000);
     };
     // read the transposed segments back and store them: line byte offset lo (+ the query image)
-    auto store_lines = [&](__amdgpu_buffer_rsrc_t rs, int64_t lsz, int ql, int lo, bool ok) {
+    auto store_lines = [&](const char* xp, __amdgpu_buffer_rsrc_t rs, int64_t lsz, int ql, int lo, bool ok) {
         floatx4 pc[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) pc[s] = *reinterpret_cast<const floatx4*>(xp + ro + s * XS);
@@ -364,7 +367,6 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
         float l1[2][4][2], l2[2][2], l3[2];
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
-            __builtin_amdgcn_sched_barrier(0);
             // scaled values of lines j = 2 bb + jl, [jl][g4][t]; target exponents
             // ext[32 j + 8 g4 + 4 arow + t]
             float v[2][4][4];
@@ -385,15 +387,15 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
             // level 0: line j = rows g4 x this lane's 4 columns
 #pragma unroll
             for (int jl = 0; jl < 2; ++jl) {
-                __builtin_amdgcn_sched_barrier(0);
                 const int j = 2 * bb + jl;
+                char* const xp = xw + j * (32 * XS);
 #pragma unroll
                 for (int g4 = 0; g4 < 4; ++g4)
                     *reinterpret_cast<floatx4*>(xp + wo + 32 * g4 + 16 * arow) =
                         floatx4{v[jl][g4][0], v[jl][g4][1], v[jl][g4][2], v[jl][g4][3]};
                 const int tr = (tc.ty0 >> 2) + (tc.band ? 0 : (j & 1));
                 const int tcl = (tc.tx0 >> 3) + (tc.band ? j : (j >> 1));
-                store_lines(r0, P.lsz[0], ql, ((tr * P.lntx[0] + tcl) * kTile) * 4 + 64 * arow,
+                store_lines(xp, r0, P.lsz[0], ql, ((tr * P.lntx[0] + tcl) * kTile) * 4 + 64 * arow,
                             tr < P.lnty[0] && tcl < P.lntx[0]);
             }
             if (L < 2) continue;
@@ -454,6 +456,7 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
         }
         // level 1 (regular: the n-tile's 4 x 8 level-1 pixels = one tile line; band: rows 0-1 of
         // two tile lines u = 0, 1, whose segment 0 the lanes acol / acol + 32 store)
+        char* const xp = xw;
         if (!tc.band) {
 #pragma unroll
             for (int bb = 0; bb < 2; ++bb)
@@ -472,7 +475,7 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
         }
         const int r1t = tc.ty0 >> 3;                                   // level-1 tile row
         const int c1t = (tc.tx0 >> 4) + (tc.band ? arow : 0);          // level-1 tile col
-        store_lines(r1, P.lsz[1], ql, ((r1t * P.lntx[1] + c1t) * kTile) * 4 + (tc.band ? 0 : 64 * arow),
+        store_lines(xp, r1, P.lsz[1], ql, ((r1t * P.lntx[1] + c1t) * kTile) * 4 + (tc.band ? 0 : 64 * arow),
                     r1t < P.lnty[1] && c1t < P.lntx[1]);
     }
 }

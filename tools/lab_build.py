@@ -122,7 +122,21 @@ PATCHES["loopstamps"] = [
      "g_stamps[blockIdx.x][2] = __builtin_amdgcn_s_memtime() - tl0; } g_stamps[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime() - tr0; }\n"),
     ("build.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + STAMP_EXPORT),
 ]
-COMBOS = {}
+# epilogue stores issued with out-of-range offsets (TA work, no memory traffic) / not issued at all
+PATCHES["epioob"] = [("build.hip", "                                                   ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_SC1);",
+                      "                                                   SOOB, 0, ST_SC1);"),
+                     ("build.hip", "        const int off = (int)((qloc * P.lsz[lv] + level_off(r, c, P.lntx[lv], P.lw[lv])) * 4);",
+                      "        const int off = SOOB; (void)qloc;")]
+PATCHES["epinost"] = [("build.hip", """            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, pc[s]), rs,
+                                                   ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_SC1);""",
+                       """            asm volatile("" :: "v"(pc[s]), "v"(ok ? base + (int)(s * lsz * 4) : SOOB));"""),
+                      ("build.hip", "    auto store_px = [&](__amdgpu_buffer_rsrc_t rs, int lv, int qloc, int r, int c, auto val) {",
+                       "    auto store_px = [&](__amdgpu_buffer_rsrc_t rs, int lv, int qloc, int r, int c, auto val) {\n        asm volatile(\"\" :: \"v\"(val), \"v\"(qloc + r + c)); return;")]
+PATCHES["prio"] = [("build.hip", "    // ---------------- epilogue (per wave, from registers) ----------------\n",
+                     "    // ---------------- epilogue (per wave, from registers) ----------------\n    __builtin_amdgcn_s_setprio(2);\n")]
+PATCHES["prio3"] = [("build.hip", "    // ---------------- epilogue (per wave, from registers) ----------------\n",
+                     "    // ---------------- epilogue (per wave, from registers) ----------------\n    __builtin_amdgcn_s_setprio(3);\n")]
+COMBOS = {"stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
 
 
 def build(name):

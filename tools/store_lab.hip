@@ -36,10 +36,9 @@ __device__ __forceinline__ void st(float* p, float v, char* gbase) {
 // one wave item = 64 images x 8 lines (64 KB); block = 4 waves
 template <int PAT, int NT>
 __global__ __launch_bounds__(256) void store_kernel(char* buf, float val) {
-    const int lane = threadIdx.x & 63;
-    const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  for (int item = blockIdx.x * 4 + (threadIdx.x >> 6); item < (NIMG / 64) * (LINES / 8); item += gridDim.x * 4) {
     const int ig = item / (LINES / 8), lr = item % (LINES / 8);
-    if (ig * 64 >= NIMG) return;
     char* base = buf + (size_t)ig * 64 * IMG_B + (size_t)lr * 8 * 128;
     const floatx4 v = {val, val + 1, val + 2, val + 3};
     if (PAT == 0) {   // coal
@@ -71,12 +70,14 @@ __global__ __launch_bounds__(256) void store_kernel(char* buf, float val) {
             for (int L = 0; L < 8; ++L)
                 st<NT>(reinterpret_cast<float*>(base + (size_t)(2 * i + h) * IMG_B + L * 128 + w * 4), val, buf);
     }
+  }
 }
 
+int g_blocks = 0;
 template <int PAT, int NT>
 float run(char* buf, int reps) {
     const int items = (NIMG / 64) * (LINES / 8);
-    const dim3 grid((items + 3) / 4);
+    const dim3 grid(g_blocks > 0 ? g_blocks : (items + 3) / 4);
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
@@ -92,6 +93,18 @@ float run(char* buf, int reps) {
 
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 10;
+    if (argc > 2) {   // per-CU rate: oct128 nt|sc1 and plain with a limited number of blocks
+        char* b2;
+        if (hipMalloc(&b2, (size_t)NIMG * IMG_B) != hipSuccess) return 1;
+        const double mv = (double)NIMG * LINES * 128;
+        for (int nb : {32, 64, 128, 256, 512, 1024, 2048}) {
+            g_blocks = nb;
+            const float a = run<1, 18>(b2, reps), c = run<1, 0>(b2, reps), d = run<0, 18>(b2, reps);
+            printf("blocks %5d: oct128 nt|sc1 %7.0f GB/s  plain %7.0f  coal nt|sc1 %7.0f\n", nb, mv / (a * 1e-3) / 1e9,
+                   mv / (c * 1e-3) / 1e9, mv / (d * 1e-3) / 1e9);
+        }
+        return 0;
+    }
     char* buf;
     const size_t bytes = (size_t)NIMG * IMG_B;
     if (hipMalloc(&buf, bytes) != hipSuccess) { printf("alloc failed\n"); return 1; }
