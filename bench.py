@@ -53,7 +53,6 @@ def parse():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-next", action="store_true", help="skip the SURVEY §8f next-row measurements")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     a = ap.parse_args()
     if a.mode == "batch":
         a.batch, a.height, a.width = a.batch or 16, a.height or 60, a.width or 80
@@ -100,47 +99,61 @@ def make_inputs(B, D, H, W, iters, device, seed):
     return f1, f2, coords
 
 
-def cpu_baseline(B, D, H, W, iters, seconds):
-    """torch-CPU restatement of the reference (oracle/torch_ref.py), bounded sample."""
+def cpu_baseline(f1, f2, coords, iters):
+    """the reference's CPU path on this host's cores, at the C1 shape (B = 1, DSEC
+    256 x 60 x 80, build + 12 lookups) on the GPU leg's own first pair (same PRNG inputs, copied to
+    the host).  Two restatements of the reference, both bit-checked against its goldens:
+      torch: oracle/torch_ref.py -- the reference's own ATen op sequence (corr.py, utils.py), on
+             all cores and on 1 core (main.py:2-5 pins the reference to one thread);
+      c:     oracle/ecorr_oracle.c -- the C restatement (fp64-accumulated GEMM), OpenMP on all cores.
+    Each leg: one warm-up, then the median of 3 timed runs."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from torch_ref import TorchCpuCorrBlock
+    import oracle
     cores = len(os.sched_getaffinity(0))
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
-    torch.set_num_threads(cores)
-    nb = min(B, 4)
-    g = torch.Generator().manual_seed(7)
-    f1 = torch.randn((nb, D, H, W), generator=g)
-    f2 = torch.randn((nb, D, H, W), generator=g)
-    ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
-    base = torch.stack([xs, ys]).float()[None].repeat(nb, 1, 1, 1)
-    coords = [base + 3.0 * torch.randn((nb, 2, H, W), generator=g) for _ in range(iters)]
+    a, b = f1[:1].cpu(), f2[:1].cpu()
+    cs = [c[:1].cpu() for c in coords]
+    an, bn, csn = a.numpy(), b.numpy(), [c.numpy() for c in cs]
 
-    def step():
-        blk = TorchCpuCorrBlock(f1, f2)
-        for c in coords:
+    def med3(fn):
+        fn()
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[1]
+
+    def torch_step():
+        blk = TorchCpuCorrBlock(a, b)
+        for c in cs:
             blk(c)
 
-    step()  # warm-up
-    pairs, t0 = 0, time.perf_counter()
-    while True:
-        step()
-        pairs += nb
-        el = time.perf_counter() - t0
-        if el >= seconds or pairs >= 64:
-            break
-    # the reference's own setting: main.py:2-5 pins torch to one thread
-    torch.set_num_threads(1)
-    blk1 = TorchCpuCorrBlock(f1[:1], f2[:1])
-    t1 = time.perf_counter()
-    for c in coords:
-        blk1(c[:1])
-    one = time.perf_counter() - t1
+    def c_step():
+        levels = oracle.pyramid_from_level0(oracle.corr_level0(an, bn), 4)
+        for c in csn:
+            oracle.lookup(levels, c, 4)
+
+    nt = torch.get_num_threads()
     torch.set_num_threads(cores)
-    return {"value": pairs / el, "unit": "pairs/s", "cores": cores, "kind": "port",
-            "sample": f"{pairs} pairs ({nb} per step, fmap {D}x{H}x{W}, build + {iters} lookups) in "
-                      f"{el:.1f} s; torch {torch.__version__} CPU ops = the reference's ATen ops",
-            "one_core": {"value": round(1.0 / one, 3), "unit": "pairs/s", "cores": 1,
-                         "sample": "1 pair, build + 12 lookups, torch.set_num_threads(1) as main.py:2-5"}}
+    t_all = med3(torch_step)
+    torch.set_num_threads(1)
+    t_one = med3(torch_step)
+    torch.set_num_threads(nt)
+    t_c = med3(c_step)   # OpenMP threads = OMP_NUM_THREADS (the box: 16)
+    shape = f"B=1, fmap {a.shape[1]}x{a.shape[2]}x{a.shape[3]}, build + {iters} lookups"
+    return {"value": round(1.0 / t_all, 3), "unit": "pairs/s", "cores": cores, "kind": "port",
+            "batch": 1, "median_of": 3,
+            "sample": f"C1: {shape}, the GPU leg's first pair; torch {torch.__version__} CPU ATen ops = the "
+                      f"reference's op sequence (oracle/torch_ref.py), {cores} threads; median of 3 after a warm-up",
+            "legs": {
+                "torch_all_cores": {"pairs_per_s": round(1.0 / t_all, 3), "s_per_pair": round(t_all, 4), "cores": cores},
+                "torch_1_core": {"pairs_per_s": round(1.0 / t_one, 3), "s_per_pair": round(t_one, 4), "cores": 1,
+                                 "note": "torch.set_num_threads(1) as main.py:2-5"},
+                "c_oracle": {"pairs_per_s": round(1.0 / t_c, 3), "s_per_pair": round(t_c, 4),
+                             "cores": int(os.environ.get("OMP_NUM_THREADS", cores)),
+                             "note": "oracle/ecorr_oracle.c, fp64-accumulated GEMM, OpenMP"}}}
 
 
 def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
@@ -296,17 +309,48 @@ def measure_voxel(device, n=1_000_000, C=15, H=480, W=640, reps=5):
 
 
 def pmc_traffic(kernel_prefix):
-    """HBM bytes per dispatch of the dominant kernel from the committed PMC summary of this same
-    bench command (profiles/latest_pmc.json, written by tools/pmc_summary.py), else None."""
+    """HBM bytes per dispatch of the dominant kernel from the committed PMC summary
+    (profiles/latest_pmc.json, tools/pmc_summary.py), used only when its kernel-source digest is
+    this tree's (a summary of other kernels is refused, not reported)."""
+    import eraft_amd
     path = os.path.join(ROOT, "profiles", "latest_pmc.json")
     try:
         js = json.load(open(path))
     except (OSError, ValueError):
-        return None, None
+        return None, "no profiles/latest_pmc.json"
+    here = eraft_amd._lib.source_digest()
+    if js.get("source_digest") != here:
+        return None, f"refused: profiles/latest_pmc.json measured sources {js.get('source_digest')}, tree is {here}"
     for name, rec in js.get("kernels", {}).items():
         if name.startswith(kernel_prefix) and "hbm_bytes" in rec:
-            return rec["hbm_bytes"], f"{js.get('source', path)}: {name} ({rec.get('read_correction')})"
-    return None, None
+            return rec["hbm_bytes"], f"{js.get('source', path)}: {name} ({rec.get('read_correction')}), sources {here}"
+    return None, f"no {kernel_prefix} record in profiles/latest_pmc.json"
+
+
+def measure_fp32_build(f1, f2, reps=5):
+    """The fp32-MFMA build (ecorr_build: v_mfma_f32_32x32x2_f32, an exact fmaf chain per element)
+    on the same inputs, outside the headline timed region: median of reps, HIP events."""
+    import eraft_amd
+    from eraft_amd import _lib
+    B, D, H, W = f1.shape
+    _, _, off = _lib.layout(B * H * W, H, W, 4)
+    stream = torch.cuda.current_stream(f1.device)
+    ts = []
+    for _ in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        _lib.build_pyramid(f1, f2, B, D, H, W, H * W, 4, off, "fp32 build", mode="fp32")
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ms = sorted(ts[1:])[len(ts[1:]) // 2]
+    flops = 2.0 * B * (H * W) ** 2 * D
+    tf = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4), "ms_per_launch": round(ms, 4),
+            "mode": "fp32", "covers": "build_kernel (v_mfma_f32_32x32x2_f32, one launch)",
+            "note": "north_star's fp32-MFMA design; the headline uses the split build (more accurate vs fp64, "
+                    "tests/test_build_modes_gpu.py)"}
 
 
 def main():
@@ -369,6 +413,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+        eraft_amd._lib.stage_events = stages = []   # split build: events around its two launches
         t0 = time.perf_counter()
         for k in range(a.steps):
             step(evs[k])
@@ -377,46 +422,67 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        eraft_amd._lib.stage_events = None
 
     build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps
     look_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps / iters
+    pack_ms = sum(e[0].elapsed_time(e[1]) for e in stages) / len(stages) if stages else 0.0
+    gemm_ms = sum(e[1].elapsed_time(e[2]) for e in stages) / len(stages) if stages else build_ms
     if distributed:
-        t = torch.tensor([elapsed, build_ms, look_ms], dtype=torch.float64,
+        t = torch.tensor([elapsed, build_ms, look_ms, pack_ms, gemm_ms], dtype=torch.float64,
                          device="cpu" if single else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, build_ms, look_ms = t.tolist()
+        elapsed, build_ms, look_ms, pack_ms, gemm_ms = t.tolist()
 
     flops, build_bytes, look_bytes = algorithmic(B, D, H, W, q=q_local)
     mode = eraft_amd._lib.build_mode()
     t_mfma, t_hbm, mfma_peak = build_floors(flops, build_bytes, mode)
-    build_tf = flops / (build_ms * 1e-3) / 1e12
-    build_gbs = build_bytes / (build_ms * 1e-3) / 1e9
-    look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
     note = "" if a.mode == "batch" else " (per rank; lookup time includes the output all-gather)"
-    mfma_roof = {"bound": "mfma", "achieved": round(build_tf, 2), "peak": round(mfma_peak, 1), "unit": "TFLOP/s",
-                 "frac": round(build_tf / mfma_peak, 4), "work_per_launch": f"{flops:.4g} flop" + note}
-    hbm_roof = {"bound": "hbm", "achieved": round(build_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(build_gbs / PEAK_HBM_GBS, 4),
-                "work_per_launch": f"{build_bytes:.4g} B (fmaps in + pyramid out)" + note}
-    # the build's binding roof is the one with the longer ideal time (fp32 MFMA: the matrix
-    # cores; split: HBM, the 1.96 GB pyramid store outweighs 3 f16 MFMAs per product)
-    bind, other = (mfma_roof, hbm_roof) if t_mfma >= t_hbm else (hbm_roof, mfma_roof)
-    kernels = {
-        "build": dict(bind, ms_per_launch=round(build_ms, 4), mode=mode,
-                      covers=("pack_both_kernel (both operand passes, one launch) + build_kernel (one CorrBlock build; "
-                              "HIP events on the launch stream)") if mode == "split" else "build_kernel",
-                      other_roof={k: other[k] for k in ("bound", "achieved", "peak", "unit", "frac")}),
-        "lookup": {"bound": "hbm", "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                   "frac": round(look_gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(look_ms, 4),
-                   "launches_per_step": iters, "work_per_launch": f"{look_bytes:.4g} B" + note},
-    }
-    dom = "build" if build_ms >= look_ms * iters else "lookup"
+
+    def roofs(ms):
+        tf, gbs = flops / (ms * 1e-3) / 1e12, build_bytes / (ms * 1e-3) / 1e9
+        m = {"bound": "mfma", "achieved": round(tf, 2), "peak": round(mfma_peak, 1), "unit": "TFLOP/s",
+             "frac": round(tf / mfma_peak, 4), "work_per_launch": f"{flops:.4g} flop" + note}
+        h = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+             "frac": round(gbs / PEAK_HBM_GBS, 4),
+             "work_per_launch": f"{build_bytes:.4g} B (fmaps in + pyramid out)" + note}
+        # binding roof = the longer ideal time (split: HBM, the 1.96 GB pyramid store outweighs 3 f16
+        # MFMAs per product; fp32: the fp32 matrix cores)
+        return (m, h) if t_mfma >= t_hbm else (h, m)
+
+    look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
+    kernels = {}
+    if mode == "split":
+        bind, other = roofs(gemm_ms)
+        wbind, _ = roofs(build_ms)
+        kernels["build"] = dict(bind, ms_per_launch=round(gemm_ms, 4), mode=mode,
+                                covers="build_split_kernel alone (GEMM + fused pyramid; HIP events on the launch stream "
+                                       "around its launch inside the timed region)",
+                                other_roof={k: other[k] for k in ("bound", "achieved", "peak", "unit", "frac")},
+                                window={"ms": round(build_ms, 4), "frac": wbind["frac"], "achieved": wbind["achieved"],
+                                        "covers": "pack_both_kernel + build_split_kernel (the whole CorrBlock build)"})
+        kernels["pack"] = {"ms_per_launch": round(pack_ms, 4), "covers": "pack_both_kernel (operand pass)",
+                           "bound": "hbm", "work_per_launch": f"{4.0 * B * D * (q_local + H * W) * 2:.4g} B "
+                                                             "(fmaps in, f16 hi/lo panels out)"}
+    else:
+        bind, other = roofs(build_ms)
+        kernels["build"] = dict(bind, ms_per_launch=round(build_ms, 4), mode=mode, covers="build_kernel",
+                                other_roof={k: other[k] for k in ("bound", "achieved", "peak", "unit", "frac")})
+    kernels["lookup"] = {"bound": "hbm", "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(look_gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(look_ms, 4),
+                         "launches_per_step": iters, "work_per_launch": f"{look_bytes:.4g} B" + note}
+    if mode == "split" and a.mode == "batch" and world == 1 and not a.no_next:
+        with torch.no_grad():
+            kernels["build_fp32"] = measure_fp32_build(f1, f2)
+    dom = "build" if gemm_ms >= look_ms * iters else "lookup"
     roof = {k: kernels[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")}
-    roof["kernel"] = dom
-    traffic, src = pmc_traffic("build_kernel" if dom == "build" else "lookup_cols")
+    roof["kernel"] = "build_split_kernel" if (dom == "build" and mode == "split") else \
+        ("build_kernel" if dom == "build" else "lookup_cols_reg")
+    if dom == "build" and mode == "split":
+        roof["window_frac"] = kernels["build"]["window"]["frac"]
+    traffic, src = pmc_traffic(roof["kernel"])
     roof["traffic"] = traffic
-    if src:
-        roof["traffic_source"] = src
+    roof["traffic_source"] = src
     ideal_s = max(t_mfma, t_hbm) + iters * look_bytes / (PEAK_HBM_GBS * 1e9)
     pairs = (world * B if a.mode == "batch" else B) * a.steps
     if a.mode == "batch":
@@ -452,7 +518,7 @@ def main():
                                 "upsample_flow": measure_upsample(B, H, W, device),
                                 "voxel_grid_dsec": measure_voxel(device)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(B, D, H, W, iters, a.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(f1, f2, coords, iters)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if distributed:

@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -40,6 +40,10 @@ SYMBOLS = {
     "ecorr_build_split_workspace_size": (_i, [_i, _i, _i, _i, _i, ctypes.POINTER(_i64)]),
     # (fmap1, fmap2, B, D, H, W, q_count, levels, pyramid, workspace, stream)
     "ecorr_build_split": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+    # (fmap1, fmap2, B, D, H, W, q_count, workspace, stream)
+    "ecorr_build_split_pack": (_i, [_p, _p, _i, _i, _i, _i, _i, _p, _p]),
+    # (B, D, H, W, q_count, levels, pyramid, workspace, stream)
+    "ecorr_build_split_gemm": (_i, [_i, _i, _i, _i, _i, _i, _p, _p, _p]),
     # (pyramid, coords, B, H, W, q_count, levels, radius, out, stream)
     "ecorr_lookup": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
     # (pyramid, coords, B, H, W, q_count, levels, radius, weight[O][C], bias, O, out, stream)
@@ -90,6 +94,21 @@ def lib():
     return _lib
 
 
+def source_digest() -> str:
+    """sha256 (16 hex) of the kernel sources and the C header: ties a committed PMC summary
+    (profiles/latest_pmc.json, tools/pmc_summary.py) to the code it measured."""
+    import hashlib
+    root = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(os.path.join(root, "csrc", f) for f in os.listdir(os.path.join(root, "csrc"))
+                   if f.endswith((".hip", ".h")))
+    files.append(os.path.join(root, "..", "include", "ecorr.h"))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def strerror(status: int) -> str:
     return lib().ecorr_strerror(status).decode()
 
@@ -126,6 +145,11 @@ if _build_mode not in BUILD_MODES:
     raise ValueError(f"ECORR_BUILD_MODE={_build_mode!r} not in {BUILD_MODES}")
 
 
+# Timing hook (bench.py): when a list, every split build appends its (start, after the operand
+# pass, after the GEMM) HIP events, recorded on the launch stream.  Never changes a result.
+stage_events = None
+
+
 def set_build_mode(mode: str):
     global _build_mode
     if mode not in BUILD_MODES:
@@ -150,8 +174,19 @@ def build_pyramid(fmap1, fmap2, B, D, H, W, q_count, levels, off, what, mode=Non
         nbytes = _i64()
         check(lib().ecorr_build_split_workspace_size(B, D, H, W, q_count, ctypes.byref(nbytes)), what)
         ws = torch.empty(nbytes.value, dtype=torch.uint8, device=fmap2.device)
-        check(lib().ecorr_build_split(fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, q_count, levels,
-                                      pyr.data_ptr(), ws.data_ptr(), st), what)
+        tm = stage_events
+        if tm is not None:   # bench.py: HIP events on this stream around the two stages
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record()
+        check(lib().ecorr_build_split_pack(fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, q_count,
+                                           ws.data_ptr(), st), what)
+        if tm is not None:
+            ev[1].record()
+        check(lib().ecorr_build_split_gemm(B, D, H, W, q_count, levels, pyr.data_ptr(), ws.data_ptr(), st),
+              what)
+        if tm is not None:
+            ev[2].record()
+            tm.append(ev)
         del ws
     else:
         check(lib().ecorr_build(fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, q_count, levels,

@@ -100,8 +100,10 @@ ECORR_EXPORT int ecorr_pyramid_formats(int H, int W, int levels, int* ntx) {
 namespace {
 
 int build_common(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count, int levels,
-                 float* pyramid, void* workspace, void* stream) {
-    if (!fmap1 || !fmap2 || !pyramid || B <= 0 || D <= 0) return ECORR_EINVAL;
+                 float* pyramid, void* workspace, void* stream, int stages = 3) {
+    if ((stages & 1) && (!fmap1 || !fmap2)) return ECORR_EINVAL;
+    if ((stages & 2) && !pyramid) return ECORR_EINVAL;
+    if (B <= 0 || D <= 0) return ECORR_EINVAL;
     if (!q_count_ok(H, W, q_count)) return ECORR_EINVAL;
     PyrGeom g;
     const int st = pyramid_geometry((int64_t)B * q_count, H, W, levels, &g);
@@ -126,7 +128,7 @@ int build_common(const float* fmap1, const float* fmap2, int B, int D, int H, in
         if (B > 65535 || ((uintptr_t)workspace & 255)) return ECORR_EINVAL;
         P.ws = static_cast<char*>(workspace);
     }
-    return launch_build(P, B, g, pyramid, (hipStream_t)stream);
+    return launch_build(P, B, g, pyramid, (hipStream_t)stream, stages);
 }
 
 }  // namespace
@@ -146,6 +148,18 @@ ECORR_EXPORT int ecorr_build_split(const float* fmap1, const float* fmap2, int B
                                    int levels, float* pyramid, void* workspace, void* stream) {
     if (!workspace) return ECORR_EINVAL;
     return build_common(fmap1, fmap2, B, D, H, W, q_count, levels, pyramid, workspace, stream);
+}
+
+ECORR_EXPORT int ecorr_build_split_pack(const float* fmap1, const float* fmap2, int B, int D, int H, int W,
+                                        int q_count, void* workspace, void* stream) {
+    if (!workspace) return ECORR_EINVAL;
+    return build_common(fmap1, fmap2, B, D, H, W, q_count, 1, nullptr, workspace, stream, 1);
+}
+
+ECORR_EXPORT int ecorr_build_split_gemm(int B, int D, int H, int W, int q_count, int levels, float* pyramid,
+                                        void* workspace, void* stream) {
+    if (!workspace) return ECORR_EINVAL;
+    return build_common(nullptr, nullptr, B, D, H, W, q_count, levels, pyramid, workspace, stream, 2);
 }
 
 namespace {

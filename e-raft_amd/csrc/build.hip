@@ -1047,7 +1047,7 @@ int64_t build_split_workspace_bytes(int B, int D, int H, int W, int q_count) {
     return split_ws(P, B).total;
 }
 
-int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid, hipStream_t stream) {
+int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid, hipStream_t stream, int stages) {
     BuildParams P = P0;
     const int levels = g.levels;
     P.fused_levels = levels < 4 ? levels : 4;
@@ -1074,7 +1074,11 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
         P.pk1 = P.ws + w.pk1;
         P.pk2 = P.ws + w.pk2;
         const int nx = 2 * (P.n_mt > P.n_nt ? P.n_mt : P.n_nt);
-        hipLaunchKernelGGL(pack_both_kernel, dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
+        if (stages & 1) hipLaunchKernelGGL(pack_both_kernel, dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
+        if (!(stages & 2)) {
+            const hipError_t e = hipGetLastError();
+            return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
+        }
         if (P.scale_is_mul) hipLaunchKernelGGL(build_split_kernel<true>, dim3((unsigned)ntiles), dim3(256), 0, stream, P);
         else hipLaunchKernelGGL(build_split_kernel<false>, dim3((unsigned)ntiles), dim3(256), 0, stream, P);
     } else {

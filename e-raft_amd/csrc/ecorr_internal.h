@@ -47,7 +47,9 @@ struct BuildParams {
     int64_t lsz[4];         // floats per query image of each fused level
 };
 
-int launch_build(const BuildParams& P, int B, const PyrGeom& g, float* pyramid, hipStream_t stream);
+// stages (split build only; the fp32 build is one launch): 1 = operand pass, 2 = GEMM + fused
+// pyramid (+ levels > 4), 3 = both
+int launch_build(const BuildParams& P, int B, const PyrGeom& g, float* pyramid, hipStream_t stream, int stages = 3);
 int64_t build_split_workspace_bytes(int B, int D, int H, int W, int q_count);
 
 struct LookupParams {

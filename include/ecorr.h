@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 9
+#define ECORR_ABI_VERSION 10
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -76,6 +76,15 @@ int ecorr_build(const float* fmap1, const float* fmap2, int B, int D, int H, int
 int ecorr_build_split_workspace_size(int B, int D, int H, int W, int q_count, int64_t* bytes);
 int ecorr_build_split(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
                       int levels, float* pyramid, void* workspace, void* stream);
+
+/* ecorr_build_split as its two stream-ordered stages, for callers that overlap or time them:
+ * _pack = the operand pass (per-pixel exponents + f16 hi/lo panels into the workspace; reads
+ * fmap1/fmap2), _gemm = the correlation GEMM with the fused pyramid (reads only the workspace).
+ * pack then gemm on one stream == ecorr_build_split, bit for bit. */
+int ecorr_build_split_pack(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
+                           void* workspace, void* stream);
+int ecorr_build_split_gemm(int B, int D, int H, int W, int q_count, int levels, float* pyramid,
+                           void* workspace, void* stream);
 
 /* Radius-r lookup: out float[B][levels*(2r+1)^2][q_count] (= [B][C][H][W] when q_count = H*W),
  * channel 81*i + 9*a + b (r = 4) = bilinear sample of level i at (x/2^i + a - r, y/2^i + b - r),

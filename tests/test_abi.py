@@ -103,6 +103,12 @@ def test_argument_validation_before_launch(ea):
     assert F(8, 8, 1, 64, 64, 4096, 5, 4, 8, None, 64, 8, None) == _lib.ECORR_ELEVELS   # levels > 4
     assert F(8, 8, 1, 16, 16, 256, 4, 4, 8, None, 96, 8, None) == _lib.ECORR_EINVAL
     assert F(8, 8, 1, 16, 16, 256, 4, 4, None, None, 64, 8, None) == _lib.ECORR_EINVAL
+    # the split build's stages validate like the whole call (no workspace / no operands)
+    assert L.ecorr_build_split_pack(8, 8, 1, 256, 8, 8, 64, None, None) == _lib.ECORR_EINVAL
+    assert L.ecorr_build_split_pack(None, 8, 1, 256, 8, 8, 64, 256, None) == _lib.ECORR_EINVAL
+    assert L.ecorr_build_split_gemm(1, 256, 8, 8, 64, 4, 8, None, None) == _lib.ECORR_EINVAL
+    assert L.ecorr_build_split_gemm(1, 256, 8, 8, 64, 4, None, 256, None) == _lib.ECORR_EINVAL
+    assert L.ecorr_build_split_gemm(1, 256, 8, 8, 65, 4, 8, 256, None) == _lib.ECORR_EINVAL
 
 
 def test_cpu_tensors_rejected_loudly(ea):
@@ -145,3 +151,13 @@ def test_split_build_arguments(ea):
     assert L.ecorr_build_split(8, 8, 1, 256, 8, 8, 64, 4, 8, None, None) == _lib.ECORR_EINVAL
     with pytest.raises(ValueError):
         _lib.set_build_mode("bf16")
+
+
+def test_pmc_source_digest_matches_library_digest(ea):
+    """bench.py ties roofline.traffic to the kernel sources a PMC summary measured; the summary
+    tool and the package must hash the same files the same way."""
+    path = os.path.join(ROOT, "tools", "pmc_summary.py")
+    src = open(path).read()
+    ns = {"__file__": path}
+    exec(compile(src.split("root = sys.argv[1]")[0], path, "exec"), ns)
+    assert ns["source_digest"]() == ea._lib.source_digest()

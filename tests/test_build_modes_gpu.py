@@ -193,3 +193,29 @@ def test_stray_dev_env_vars_change_nothing(ea, monkeypatch):
     dirty = run()
     for a, b in zip(clean, dirty):
         assert torch.equal(a, b)
+
+
+def test_split_two_stage_calls_match_one(ea):
+    """ecorr_build_split_pack + ecorr_build_split_gemm (what CorrBlock issues) == ecorr_build_split."""
+    import ctypes
+    from eraft_amd import _lib
+    B, D, H, W = 2, 256, 23, 40
+    f1 = torch.from_numpy(prng.normal(81, (B, D, H, W))).to(DEV)
+    f2 = torch.from_numpy(prng.normal(82, (B, D, H, W))).to(DEV)
+    _, _, off = _lib.layout(B * H * W, H, W, 4)
+    with torch.no_grad():
+        two = _lib.build_pyramid(f1, f2, B, D, H, W, H * W, 4, off, "two-stage", mode="split")
+        one = torch.empty_like(two)
+        nb = ctypes.c_int64()
+        _lib.check(_lib.lib().ecorr_build_split_workspace_size(B, D, H, W, H * W, ctypes.byref(nb)), "ws")
+        ws = torch.empty(nb.value, dtype=torch.uint8, device=DEV)
+        _lib.check(_lib.lib().ecorr_build_split(f1.data_ptr(), f2.data_ptr(), B, D, H, W, H * W, 4, one.data_ptr(),
+                                                ws.data_ptr(), _lib.stream_of(f1)), "one call")
+        torch.cuda.synchronize()
+    from eraft_amd.layout import formats, untile
+    h, w, _ = _lib.layout(B * H * W, H, W, 4)
+    ntx = formats(H, W, 4)
+    for i in range(4):
+        a = untile(one[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i])
+        b = untile(two[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i])
+        assert torch.equal(a, b), f"level {i}"

@@ -19,6 +19,21 @@ import json
 import os
 import sys
 
+def source_digest():
+    """Same digest as eraft_amd._lib.source_digest() (kept torch-free here): which kernel sources
+    this summary measured; bench.py refuses a summary of other sources."""
+    import hashlib
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(repo, "e-raft_amd", "csrc")
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".hip", ".h")))
+    files.append(os.path.join(repo, "include", "ecorr.h"))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 root = sys.argv[1]
 out = sys.argv[2] if len(sys.argv) > 2 else None
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -28,7 +43,7 @@ for f in sorted(glob.glob(os.path.join(root, "pmc*", "*counter_collection.csv"))
         if "ecorr" not in name:
             continue
         name = name.replace("void ", "").replace("ecorr::(anonymous namespace)::", "")
-        name = name.split("(ecorr")[0].split("(int")[0].split("(float")[0]
+        name = name.split("(ecorr")[0].split("(int")[0].split("(float")[0].split("(LookupParams")[0]
         agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 lines = ["# per-dispatch averages (FETCH_SIZE / WRITE_SIZE in KiB as reported; gfx950 FETCH_SIZE reads",
          "# ~1/2 of wide streaming bytes, MI355X_MICROARCH.md §HBM)"]
@@ -54,4 +69,5 @@ print(txt)
 if out:
     os.makedirs(out, exist_ok=True)
     open(os.path.join(out, "pmc_summary.txt"), "w").write(txt + "\n")
-    json.dump({"source": root, "kernels": js}, open(os.path.join(out, "pmc_summary.json"), "w"), indent=1)
+    json.dump({"source": root, "source_digest": source_digest(), "kernels": js},
+              open(os.path.join(out, "pmc_summary.json"), "w"), indent=1)
