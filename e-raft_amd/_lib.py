@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -50,6 +50,8 @@ SYMBOLS = {
     "ecorr_lookup_conv1x1_relu": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _p, _p]),
     "ecorr_bilinear_sampler": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _p]),
     "ecorr_coords_grid": (_i, [_i, _i, _i, _p, _p]),
+    # (chunks, chunk, world, B, C, H, W, out, stream)
+    "ecorr_rows_assemble": (_i, [_p, _i64, _i, _i, _i, _i, _i, _p, _p]),
     "ecorr_pyramid_tile": (_i, [ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     # (H, W, levels, ntx[levels])
     "ecorr_pyramid_formats": (_i, [_i, _i, _i, ctypes.POINTER(_i)]),

@@ -106,6 +106,8 @@ class CorrBlock:
         _no_grad_inputs(coords, weight, *(() if bias is None else (bias,)))
         if tuple(coords.shape) != (B, 2, H, W):
             raise RuntimeError(f"coords shape {tuple(coords.shape)} != {(B, 2, H, W)} of the pyramid")
+        if any(t.device != self._device for t in (coords, weight, *(() if bias is None else (bias,)))):
+            raise RuntimeError("coords / weight / bias are on a different device than the pyramid")
         K = 2 * self.radius + 1
         C = self.num_levels * K * K
         O = weight.shape[0]

@@ -223,6 +223,14 @@ ECORR_EXPORT int ecorr_coords_grid(int B, int H, int W, float* out, void* stream
     return launch_coords_grid(B, H, W, out, (hipStream_t)stream);
 }
 
+ECORR_EXPORT int ecorr_rows_assemble(const float* chunks, int64_t chunk, int world, int B, int C, int H, int W,
+                                     float* out, void* stream) {
+    if (!chunks || !out || world < 1 || B <= 0 || C <= 0 || H < world || W <= 0) return ECORR_EINVAL;
+    const int64_t rows_max = H / world + (H % world ? 1 : 0);
+    if (chunk < (int64_t)B * C * rows_max * W || (int64_t)B * C > 0x7fffffff) return ECORR_EINVAL;
+    return launch_rows_assemble(chunks, chunk, world, B, C, H, W, out, (hipStream_t)stream);
+}
+
 namespace {
 
 bool splat_dims_ok(int B, int64_t n, int h, int w) {

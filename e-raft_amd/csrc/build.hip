@@ -37,6 +37,17 @@ __device__ __forceinline__ float pool4(float a, float b, float c, float d) {
     return __fmul_rn(__fadd_rn(__fadd_rn(__fadd_rn(a, b), c), d), 0.25f);
 }
 
+// pool4 as four VALU ops in the same order: left to itself hipcc pairs the split epilogue's pools
+// into v_pk_add_f32 whose operands sit in different register pairs (two v_mov per packed add)
+__device__ __forceinline__ float pool4_v(float a, float b, float c, float d) {
+    float s;
+    asm("v_add_f32 %0, %1, %2" : "=v"(s) : "v"(a), "v"(b));
+    asm("v_add_f32 %0, %1, %2" : "=v"(s) : "v"(s), "v"(c));
+    asm("v_add_f32 %0, %1, %2" : "=v"(s) : "v"(s), "v"(d));
+    asm("v_mul_f32 %0, 0.25, %1" : "=v"(s) : "v"(s));
+    return s;
+}
+
 // 2^e as a float, e in [-126, 127]
 __device__ __forceinline__ float exp2i(int e) { return __int_as_float((e + 127) << 23); }
 
@@ -133,13 +144,15 @@ __device__ __forceinline__ float* level_px(const BuildParams& P, int L, int64_t 
 // writes 8 whole 128-byte lines.  Levels 2-3 (6% of the bytes) are single pixels, plain stores.
 // ============================================================================================
 constexpr int SQ = 256;                     // queries per split tile
-constexpr int SCHUNK = 3 * PANEL;           // LDS bytes per K chunk (2 query panels + 1 target panel)
+constexpr int SCHUNK = PANEL;               // LDS bytes per K chunk (the target panel)
 constexpr int SNBUF = 3;
-constexpr int SCOPIES = SCHUNK / 1024 / 4;  // LDS-DMA copies per wave per chunk (6)
+constexpr int SCOPIES = SCHUNK / 1024 / 4;  // LDS-DMA copies per wave per chunk (2)
+constexpr int QLOADS = 4;                   // query fragment loads per wave per chunk (hi, lo x 2 rows)
+constexpr int SLDS = 4 * 4 * 32 * 144;      // LDS bytes: the epilogue's transpose regions (> the K loop's)
 constexpr int SOOB = 0x7ffffff0;            // buffer offset beyond any panel: loads 0, touches nothing
 constexpr int ST_SC1 = 18;                  // level-0/1 store cache policy: nt sc1 (write through, drop from L2)
 constexpr int XS = 144;                     // LDS bytes per query of the epilogue's line transpose
-static_assert(4 * 4 * 32 * XS <= SNBUF * SCHUNK, "epilogue transpose regions fit the chunk buffers");
+static_assert(4 * 4 * 32 * XS <= SLDS && SNBUF * SCHUNK <= SLDS, "LDS regions");
 
 // target (y, x) of position p of a split fmap2 panel, relative to the n-tile origin
 __host__ __device__ __forceinline__ void split_target(int p, bool band, int& y, int& x) {
@@ -159,13 +172,17 @@ __device__ __forceinline__ void swap32(float& a, float& b) {
     b = __uint_as_float(r[1]);
 }
 
-template <bool MUL>
+// NK: K chunks known at compile time (16: D = 256, the E-RAFT feature width) -- the K loop is then
+// fully unrolled, which lets hipcc count the in-flight query loads exactly (in the rolled loop it
+// drains them at the loop header); 0 = any D.
+template <bool MUL, int NK>
 __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
     // ALL LDS in this one array: a second __shared__ object can make hipcc wait vmcnt(0) before
     // every ds_read while a buffer_load ... lds is in flight (cdna_hip_programming.md trap 4(a))
-    __shared__ __attribute__((aligned(16))) char smem[SNBUF * SCHUNK + (SQ + 128) * 4];
-    int* exq = reinterpret_cast<int*>(smem + SNBUF * SCHUNK);   // exponents of the 256 queries
-    int* ext = exq + SQ;                                        // ... and of the 128 panel targets
+    __shared__ __attribute__((aligned(16))) char smem[SLDS + (SQ + 256) * 4];
+    int* exq = reinterpret_cast<int*>(smem + SLDS);             // exponents of the 256 queries
+    int* ext = exq + SQ;                                        // ... negated, of the 128 panel targets
+    float* fst = reinterpret_cast<float*>(ext + 128);           // 2^ext when |ext| <= 63
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int acol = lane & 31, arow = lane >> 5;
@@ -184,12 +201,14 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
             split_target(tid, tc.band, y, x);
             y += tc.ty0;
             x += tc.tx0;
-            ext[tid] = (y < H && x < W) ? P.ex2[(int64_t)b * Q + (int64_t)y * W + x] : 0;
+            const int e = (y < H && x < W) ? -P.ex2[(int64_t)b * Q + (int64_t)y * W + x] : 0;
+            ext[tid] = e;
+            fst[tid] = exp2i(max(-63, min(e, 63)));
         }
     }
 
     // ---- operand panels of this tile: two query panels (adjacent tiles of pk1), one target panel
-    const int dc = (P.D + 15) / 16, nk = dc;
+    const int dc = (P.D + 15) / 16, nk = NK ? NK : dc;
     const int64_t pstride = (int64_t)dc * PANEL;   // bytes of one 128-pixel tile's panels
     const int qp = 2 * qt;
     const int nqp = min(2, P.n_mt - qp);
@@ -197,23 +216,16 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
         const_cast<char*>(P.pk1 + ((int64_t)b * P.n_mt + qp) * pstride), 0, (int)(nqp * pstride), 0x00020000);
     const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<char*>(P.pk2 + ((int64_t)b * P.n_nt + nt) * pstride), 0, (int)pstride, 0x00020000);
-    // copy s of this wave: 1-KB piece c = wave + 4 s of the chunk (pieces 0-15: query panels, 16-23:
-    // the target panel); lane-linear, as LDS-DMA requires
+    // target panel: copy s of this wave = 1-KB piece wave + 4 s of the chunk (lane-linear, as
+    // LDS-DMA requires)
     auto issue = [&](int kc) {
         char* dst = smem + (kc % SNBUF) * SCHUNK;
         const bool in = kc < nk;
 #pragma unroll
         for (int s = 0; s < SCOPIES; ++s) {
             const int c = wave + 4 * s;
-            if (s < 4) {
-                const int off = (c >> 3) * (int)pstride + kc * PANEL + (c & 7) * 1024 + lane * 16;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rq, (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, in ? off : SOOB, 0, 0, 0);
-            } else {
-                const int off = kc * PANEL + (c - 16) * 1024 + lane * 16;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rt, (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, in ? off : SOOB, 0, 0, 0);
-            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + c * 1024), 16,
+                                                     in ? kc * PANEL + c * 1024 + lane * 16 : SOOB, 0, 0, 0);
         }
     };
 
@@ -231,74 +243,116 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
 
-    // fragments of one chunk: query i hi/lo (query panel wave/2, 32-row group 2 (wave&1) + i),
-    // target j hi/lo (target panel, group j); panel group = [hi k0-15 | lo k0-15] x 32 rows, 16 B
-    // per lane
-    const int qfo = (wave >> 1) * PANEL + (wave & 1) * 4096 + lane * 16;
-    const int tfo = 2 * PANEL + lane * 16;
-    struct Frags { halfx8 qh[2], ql[2], th[4], tl[4]; };
-    auto read_lo = [&](int kc, Frags& f) {   // what the lo*hi MFMAs need: ql, th
-        const char* cb = smem + (kc % SNBUF) * SCHUNK;
+    // query fragments: wave-private (rows 64 wave .. + 63), so they go global -> VGPR directly,
+    // one chunk ahead: query panel wave/2, 32-row group 2 (wave&1) + i, [hi | lo] 1 KB each
+    struct QFrags { halfx8 qh[2], ql[2]; };
+    const int qgo = (wave >> 1) * (int)pstride + (wave & 1) * 4096 + lane * 16;
+    auto load_q = [&](int kc, QFrags& q) {
+        const bool in = kc < nk;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) f.ql[i] = *reinterpret_cast<const halfx8*>(cb + qfo + i * 2048 + 1024);
+        for (int i = 0; i < 2; ++i) {
+            q.qh[i] = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rq, in ? qgo + kc * PANEL + i * 2048 : SOOB, 0, 0));
+            q.ql[i] = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rq, in ? qgo + kc * PANEL + i * 2048 + 1024 : SOOB, 0, 0));
+        }
+    };
+    // target fragments of one chunk from LDS: group j, [hi k0-15 | lo k0-15] x 32 rows, 16 B per lane
+    const int tfo = lane * 16;
+    struct TFrags { halfx8 th[4], tl[4]; };
+    auto read_lo = [&](int kc, TFrags& f) {   // what the lo*hi MFMAs need besides ql: th
+        const char* cb = smem + (kc % SNBUF) * SCHUNK;
 #pragma unroll
         for (int j = 0; j < 4; ++j) f.th[j] = *reinterpret_cast<const halfx8*>(cb + tfo + j * 2048);
     };
-    auto read_hi = [&](int kc, Frags& f) {   // qh, tl
+    auto read_hi = [&](int kc, TFrags& f) {   // tl
         const char* cb = smem + (kc % SNBUF) * SCHUNK;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) f.qh[i] = *reinterpret_cast<const halfx8*>(cb + qfo + i * 2048);
 #pragma unroll
         for (int j = 0; j < 4; ++j) f.tl[j] = *reinterpret_cast<const halfx8*>(cb + tfo + j * 2048 + 1024);
     };
     // per element: lo*hi, then hi*lo, then hi*hi (the accumulation order of the round-1 build)
-    auto mfma_lohi = [&](const Frags& f) {
+    auto mfma_lohi = [&](const TFrags& f, const QFrags& q) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.th[j], f.ql[i], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.th[j], q.ql[i], acc[i][j], 0, 0, 0);
     };
-    auto mfma_rest = [&](const Frags& f) {
+    auto mfma_rest = [&](const TFrags& f, const QFrags& q) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.tl[j], f.qh[i], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.tl[j], q.qh[i], acc[i][j], 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.th[j], f.qh[i], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.th[j], q.qh[i], acc[i][j], 0, 0, 0);
     };
-    // chunk j's copies landed (the chunk after it may fly), this wave's earlier fragment reads
-    // are done; the barrier publishes chunk j and retires every wave's reads of chunk j - 1, whose
-    // buffer chunk j + 2 then takes
+    // VMEM issue order per wave: t(j + 1) [in advance(j - 1)], q(j) [end of chunk j - 2], t(j + 2)
+    // [advance(j)], q(j + 1) [end of chunk j - 1], ...  advance(j) (after chunk j - 1's lo*hi
+    // MFMAs) waits until t(j) has landed, with the 6 younger t(j + 1), q(j) in flight; the
+    // compiler's own vmcnt waits cover the q registers before their MFMAs.  The barrier publishes
+    // chunk j and retires every wave's reads of chunk j - 1, whose buffer chunk j + 2 then takes
+    // Every wait count above assumes the VMEM issue order of the source, so the loads are fenced
+    // from each other and from the waits by sched_barrier (hipcc otherwise hoists the query loads
+    // over the LDS-DMA, e.g. q(0) in front of t(0) -- a race on t(0)), and the phases below stay
+    // in program order (left free, hipcc gathers each chunk's LDS reads in front of their first
+    // MFMA and exposes their latency every chunk).
+#define PHASE __builtin_amdgcn_sched_barrier(0)
     auto advance = [&](int j) {
-        wait_vm<SCOPIES, true>();
+        PHASE;
+        wait_vm<SCOPIES + QLOADS, true>();
         __builtin_amdgcn_s_barrier();
+        PHASE;
         issue(j + 2);
+        PHASE;
     };
 
-    Frags fa, fb;
+    TFrags fa, fb;
+    QFrags qa, qb;
     issue(0);
+    PHASE;
     issue(1);
-    advance(0);
+    PHASE;
+    load_q(0, qa);
+    PHASE;
+    wait_vm<SCOPIES + QLOADS, true>();   // t(0) landed (t(1), q(0) may fly)
+    __builtin_amdgcn_s_barrier();
+    PHASE;
+    issue(2);
+    PHASE;
     read_lo(0, fa);
     read_hi(0, fa);
+    PHASE;
+    load_q(1, qb);
+    PHASE;
+#pragma unroll NK ? NK : 1
     for (int kc = 0; kc < nk; kc += 2) {
-        mfma_lohi(fa);
+        mfma_lohi(fa, qa);
+        PHASE;
         advance(kc + 1);
         read_lo(kc + 1, fb);
-        mfma_rest(fa);
+        PHASE;
+        mfma_rest(fa, qa);
+        PHASE;
         read_hi(kc + 1, fb);
+        load_q(kc + 2, qa);
+        PHASE;
         if (kc + 1 >= nk) break;   // odd chunk count: fb is a zero chunk
-        mfma_lohi(fb);
+        mfma_lohi(fb, qb);
+        PHASE;
         advance(kc + 2);
         read_lo(kc + 2, fa);
-        mfma_rest(fb);
+        PHASE;
+        mfma_rest(fb, qb);
+        PHASE;
         read_hi(kc + 2, fa);
+        load_q(kc + 3, qb);
+        PHASE;
     }
+#undef PHASE
     wait_vm<0, true>();             // the trailing zero chunks have landed and this wave's reads are done ...
     __builtin_amdgcn_s_barrier();   // ... in every wave: the chunk buffers are the epilogue's scratch
 #pragma unroll
@@ -354,6 +408,20 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
                                                       r < P.lh[lv] && c + k < P.lw[lv] ? off + 4 * k : SOOB, 0, 0);
         }
     };
+    // Scaling: x = acc 2^(nqe + ext) (/ sqrt(D) when that is no power of two).  Where every
+    // exponent of the wave's queries and of the panel's targets lies in [-63, 63], the 2^nqe 2^ext
+    // product is a normal power of two and one multiply by it rounds exactly as ldexpf does: two
+    // packed multiplies per element pair instead of an add, a negate and an ldexp per element.
+    bool fast_scale;
+    {
+        bool ok = ext[lane] >= -63 && ext[lane] <= 63 && ext[lane + 64] >= -63 && ext[lane + 64] <= 63;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int n = -(exq[wave * 64 + 32 * i + acol] + (MUL ? P.scale_shift : 0));
+            ok = ok && n >= -63 && n <= 63;
+        }
+        fast_scale = __all(ok);
+    }
     const __amdgpu_buffer_rsrc_t r0 = rsrc_of(0);
     const __amdgpu_buffer_rsrc_t r1 = rsrc_of(L > 1 ? 1 : 0);
     const __amdgpu_buffer_rsrc_t r2 = rsrc_of(L > 2 ? 2 : 0);
@@ -370,17 +438,34 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
             // scaled values of lines j = 2 bb + jl, [jl][g4][t]; target exponents
             // ext[32 j + 8 g4 + 4 arow + t]
             float v[2][4][4];
+            if (fast_scale) {
+                const float sq = exp2i(nqe);
 #pragma unroll
-            for (int jl = 0; jl < 2; ++jl) {
-                const int j = 2 * bb + jl;
+                for (int jl = 0; jl < 2; ++jl) {
+                    const int j = 2 * bb + jl;
 #pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    const int4 e4 = *reinterpret_cast<const int4*>(ext + 32 * j + 8 * g4 + 4 * arow);
-                    const int e[4] = {e4.x, e4.y, e4.z, e4.w};
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        const floatx4 s4 = *reinterpret_cast<const floatx4*>(fst + 32 * j + 8 * g4 + 4 * arow);
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const float x = ldexpf(acc[i][j][4 * g4 + t], nqe - e[t]);
-                        v[jl][g4][t] = MUL ? x : __fdiv_rn(x, P.scale);
+                        for (int t = 0; t < 4; ++t) {
+                            const float x = __fmul_rn(acc[i][j][4 * g4 + t], __fmul_rn(sq, s4[t]));
+                            v[jl][g4][t] = MUL ? x : __fdiv_rn(x, P.scale);
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int jl = 0; jl < 2; ++jl) {
+                    const int j = 2 * bb + jl;
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        const int4 e4 = *reinterpret_cast<const int4*>(ext + 32 * j + 8 * g4 + 4 * arow);
+                        const int e[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const float x = ldexpf(acc[i][j][4 * g4 + t], nqe + e[t]);
+                            v[jl][g4][t] = MUL ? x : __fdiv_rn(x, P.scale);
+                        }
                     }
                 }
             }
@@ -407,16 +492,16 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
                         const int jl = y1 >> 1, g = 2 * (y1 & 1);
-                        l1[bb][y1][c] = pool4(v[jl][g][2 * c], v[jl][g][2 * c + 1], v[jl][g + 1][2 * c],
+                        l1[bb][y1][c] = pool4_v(v[jl][g][2 * c], v[jl][g][2 * c + 1], v[jl][g + 1][2 * c],
                                               v[jl][g + 1][2 * c + 1]);
                     }
                 if (L >= 3) {   // level 2: rows r, col 2 bb + arow (stored per i below)
 #pragma unroll
                     for (int r = 0; r < 2; ++r)
-                        l2[bb][r] = pool4(l1[bb][2 * r][0], l1[bb][2 * r][1], l1[bb][2 * r + 1][0], l1[bb][2 * r + 1][1]);
+                        l2[bb][r] = pool4_v(l1[bb][2 * r][0], l1[bb][2 * r][1], l1[bb][2 * r + 1][0], l1[bb][2 * r + 1][1]);
                     // level 3, the 8 x 8 pool: lane acol + 32 holds the right column
                     const float o0 = __shfl_xor(l2[bb][0], 32), o1 = __shfl_xor(l2[bb][1], 32);
-                    l3[bb] = pool4(l2[bb][0], o0, l2[bb][1], o1);
+                    l3[bb] = pool4_v(l2[bb][0], o0, l2[bb][1], o1);
                 }
             } else {
                 // band: line j = row g4 x cols 8 j + 4 arow + t; level 1 rows y1 = 0..1, cols
@@ -427,12 +512,12 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
                     for (int y1 = 0; y1 < 2; ++y1)
 #pragma unroll
                         for (int c = 0; c < 2; ++c)
-                            l1[bb][2 * y1 + jl][c] = pool4(v[jl][2 * y1][2 * c], v[jl][2 * y1][2 * c + 1],
+                            l1[bb][2 * y1 + jl][c] = pool4_v(v[jl][2 * y1][2 * c], v[jl][2 * y1][2 * c + 1],
                                                            v[jl][2 * y1 + 1][2 * c], v[jl][2 * y1 + 1][2 * c + 1]);
                 if (L >= 3) {   // level 2: col 2 (2 bb + jl) + arow (stored per i below)
 #pragma unroll
                     for (int jl = 0; jl < 2; ++jl)
-                        l2[bb][jl] = pool4(l1[bb][jl][0], l1[bb][jl][1], l1[bb][2 + jl][0], l1[bb][2 + jl][1]);
+                        l2[bb][jl] = pool4_v(l1[bb][jl][0], l1[bb][jl][1], l1[bb][2 + jl][0], l1[bb][2 + jl][1]);
                 }
             }
         }
@@ -1079,8 +1164,14 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
             const hipError_t e = hipGetLastError();
             return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
         }
-        if (P.scale_is_mul) hipLaunchKernelGGL(build_split_kernel<true>, dim3((unsigned)ntiles), dim3(256), 0, stream, P);
-        else hipLaunchKernelGGL(build_split_kernel<false>, dim3((unsigned)ntiles), dim3(256), 0, stream, P);
+        const dim3 grid((unsigned)ntiles);
+        if ((P.D + 15) / 16 == 16) {
+            if (P.scale_is_mul) hipLaunchKernelGGL((build_split_kernel<true, 16>), grid, dim3(256), 0, stream, P);
+            else hipLaunchKernelGGL((build_split_kernel<false, 16>), grid, dim3(256), 0, stream, P);
+        } else {
+            if (P.scale_is_mul) hipLaunchKernelGGL((build_split_kernel<true, 0>), grid, dim3(256), 0, stream, P);
+            else hipLaunchKernelGGL((build_split_kernel<false, 0>), grid, dim3(256), 0, stream, P);
+        }
     } else {
         const int64_t ntiles = (int64_t)B * P.n_mt * P.n_nt;
         if (ntiles <= 0 || ntiles > 0x7fffffff) return ECORR_EINVAL;

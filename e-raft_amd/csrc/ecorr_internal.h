@@ -75,6 +75,10 @@ int launch_bilinear_sampler(const float* img, int N, int C, int h, int w, const 
 
 int launch_coords_grid(int B, int H, int W, float* out, hipStream_t stream);
 
+// rows.hip: [world][chunk] all-gathered row chunks -> [B][C][H][W] (include/ecorr.h)
+int launch_rows_assemble(const float* chunks, int64_t chunk, int world, int B, int C, int H, int W, float* out,
+                         hipStream_t stream);
+
 int launch_upsample_flow(const float* flow, const float* mask, int N, int H, int W, float* out, hipStream_t stream);
 int launch_png16_encode(const float* flow, int B, int h, int w, uint16_t* out, hipStream_t stream);
 int launch_png16_decode(const uint16_t* in, int B, int h, int w, float* flow, uint8_t* valid, int* bad,

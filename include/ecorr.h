@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 10
+#define ECORR_ABI_VERSION 11
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -114,6 +114,17 @@ int ecorr_bilinear_sampler(const float* img, int N, int C, int h, int w, const f
 /* coords_grid: out float[B][2][H][W], channel 0 = x (column), 1 = y (row).
  * Replaces: model/utils.py:24-27. */
 int ecorr_coords_grid(int B, int H, int W, float* out, void* stream);
+
+/* ---- SURVEY §8e, configs[4]: the query-row sharded CorrBlock's exchange (rowshard.py) ----
+ * Reassembly after an all-gather of `world` fixed-size chunks: chunk r (floats [r*chunk,
+ * (r+1)*chunk) of `chunks`) starts with rank r's rows as float[B][C][rows_r][W], where rows_r is
+ * the contiguous near-equal partition of H (the first H % world ranks own H/world + 1 rows, rank r
+ * starts at row r*(H/world) + min(r, H % world)); the rest of the chunk is padding.  Writes
+ * out float[B][C][H][W].  chunk >= B*C*ceil(H/world)*W and H >= world (else ECORR_EINVAL).
+ * Replaces: the torch.cat reassembly of the per-iteration lookup all-gather (the reference
+ * keeps the GRU replicated, eraft.py:128-132, so every rank needs the full map). */
+int ecorr_rows_assemble(const float* chunks, int64_t chunk, int world, int B, int C, int H, int W,
+                        float* out, void* stream);
 
 /* ---- the warm-start splat (utils/image_utils.py) ----
  * Deterministic and bit-exact with the reference's serial CPU put_(accumulate=True): the scatter

@@ -1,7 +1,10 @@
 """Query-row sharded CorrBlock on the GPU: 2 ranks on cuda:0 (gloo carries CUDA tensors), each
-building only its query rows from row slabs (fmap2 all-gathered), must reproduce the unsharded
-CorrBlock bit for bit -- the per-element MFMA k order does not depend on the tiling -- and the
-gathered lookup must equal the unsharded lookup exactly."""
+building only its query rows, must reproduce the unsharded CorrBlock bit for bit -- the
+per-element MFMA k order does not depend on the tiling -- and the gathered lookup (plain 324
+channels, and fused relu(convc1(lookup)) 256 channels) must equal the unsharded one exactly.
+Cases: a ragged 23 x 40 map (12 + 11 rows) and BASELINE configs[4]'s shape, 1280 x 720 frames
+= 92 x 160 fmaps, D = 256, B = 4.  The collective here is gloo (one GPU); the RCCL branch
+(all_gather_into_tensor) runs only on multi-GPU nodes."""
 import os
 import socket
 
@@ -22,7 +25,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, shape, q):
     import sys
     for p in (ROOT, os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
@@ -32,46 +35,68 @@ def _worker(rank, world, port, q):
         import eraft_amd
         import prng
         from eraft_amd.rowshard import RowShardedCorrBlock, row_partition
-        B, D, H, W = 2, 256, 23, 40            # ragged rows: 12 + 11
+        B, D, H, W = shape
         f1 = torch.from_numpy(prng.normal(71, (B, D, H, W))).cuda()
         f2 = torch.from_numpy(prng.normal(72, (B, D, H, W))).cuda()
         coords = torch.from_numpy(prng.coords_with_flow(73, B, H, W, 4.0)).cuda()
+        wt = torch.from_numpy(prng.normal(74, (256, 324, 1, 1), 0.05)).cuda()
+        bias = torch.from_numpy(prng.normal(75, (256,), 0.1)).cuda()
         starts, counts = row_partition(H, world)
         r0, rr = starts[rank], counts[rank]
+        res = {}
         with torch.no_grad():
             full = eraft_amd.CorrBlock(f1, f2)
             ref = full(coords)
+            ref_fused = full.lookup_conv1x1_relu(coords, wt, bias)
             sh = RowShardedCorrBlock.from_row_slabs(f1[:, :, r0:r0 + rr], f2[:, :, r0:r0 + rr], H)
-            out = sh(coords)
+            for it in range(2):   # persistent exchange buffers, reused
+                res[f"plain{it}"] = bool(torch.equal(sh(coords), ref))
+                res[f"fused{it}"] = bool(torch.equal(sh.lookup_conv1x1_relu(coords, wt, bias), ref_fused))
+            res["local"] = bool(torch.equal(sh.lookup_local(coords[:, :, r0:r0 + rr].contiguous()),
+                                            ref[:, :, r0:r0 + rr]))
             rep = RowShardedCorrBlock(f1, f2)   # replicated-fmap constructor
-            out2 = rep(coords)
-        torch.cuda.synchronize()
-        rows = slice(B * 0, None)
-        lvl_ok = all(
-            torch.equal(sh.corr_pyramid[i].view(B, rr * W, -1),
-                        full.corr_pyramid[i].view(B, H * W, -1)[:, r0 * W:(r0 + rr) * W])
-            for i in range(4))
-        q.put((rank, lvl_ok, bool(torch.equal(out, ref)), bool(torch.equal(out2, ref)), None))
-        del rows
+            res["replicated"] = bool(torch.equal(rep(coords), ref))
+            torch.cuda.synchronize()
+            res["pyramid"] = all(
+                torch.equal(sh.corr_pyramid[i].view(B, rr * W, -1),
+                            full.corr_pyramid[i].view(B, H * W, -1)[:, r0 * W:(r0 + rr) * W])
+                for i in range(4))
+            # the loud contract: mismatched fmaps, coords on the wrong device / shape
+            neg = []
+            for bad in (lambda: RowShardedCorrBlock(f1, f2[:, :, :-1].contiguous()),
+                        lambda: RowShardedCorrBlock(f1, f2.cpu()),
+                        lambda: sh.lookup_local(coords[:, :, r0:r0 + rr].cpu()),
+                        lambda: sh.lookup_local(coords[:, :, :1].contiguous()),
+                        lambda: sh.lookup_conv1x1_relu(coords, wt.cpu(), bias),
+                        lambda: sh.lookup_conv1x1_relu(coords, wt[:, :100].contiguous(), bias),
+                        lambda: full.lookup_conv1x1_relu(coords, wt, bias.cpu())):
+                try:
+                    bad()
+                    neg.append(False)
+                except (RuntimeError, TypeError):
+                    neg.append(True)
+            res["negative"] = all(neg)
+        q.put((rank, res, None))
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001
-        q.put((rank, False, False, False, repr(e)))
+        q.put((rank, {}, repr(e)))
 
 
-def test_rowshard_two_ranks_bit_exact():
+@pytest.mark.parametrize("shape", [(2, 256, 23, 40), (4, 256, 92, 160)], ids=["23x40_ragged", "c5_92x160_b4"])
+def test_rowshard_two_ranks_bit_exact(shape):
     if not torch.cuda.is_available():
         pytest.fail("no HIP device visible")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, shape, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=180) for _ in procs]
+    res = [q.get(timeout=240) for _ in procs]
     for p in procs:
         p.join(timeout=60)
-    for rank, lvl_ok, out_ok, out2_ok, err in res:
+    for rank, r, err in res:
         assert err is None, err
-        assert lvl_ok, f"rank {rank}: pyramid slab differs from the unsharded pyramid"
-        assert out_ok and out2_ok, f"rank {rank}: gathered lookup differs"
-    assert np.all([r[2] for r in res])
+        bad = [k for k, v in r.items() if not v]
+        assert not bad, f"rank {rank}: {bad}"
+    assert np.all([len(r[1]) == 9 for r in res])

@@ -44,6 +44,12 @@ PATCHES = {
                  "    if (blockIdx.x >= 256 && blockIdx.x < 512)\n        for (int z = 0; z < 3; ++z) __builtin_amdgcn_s_sleep(127);\n"
                  "    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n    const int acol")],
 }
+# half-period stagger (~11 us at 1.43 GHz) of the second resident block of every CU
+PATCHES["stagger2"] = [(f, o, n.replace("z < 3", "z < 2")) for f, o, n in PATCHES["stagger"]]
+# timing only: the K loop without the 4 query-panel LDS-DMA pieces per wave and chunk (the query
+# fragments read stale LDS): what does the DMA issue cost the loop?
+PATCHES["noqdma"] = [("build.hip", "            if (s < 4) {\n", "            if (s < 4) { continue;\n"),
+                     ("build.hip", "        wait_vm<SCOPIES, true>();\n", "        wait_vm<2, true>();\n")]
 # stores spread over the K loop (4 store instructions per chunk, level-0-line shaped, junk
 # values), epilogue dropped: does spreading the store stream let it overlap the matrix work?
 SPREAD_SLOT = """
@@ -106,16 +112,16 @@ PATCHES["stamps"] = [
 PATCHES["loopstamps"] = [
     ("build.hip", "constexpr int SQ = 256; ", STAMP_DECL + "__device__ unsigned long long g_lw, g_lb;\nconstexpr int SQ = 256; "),
     ("build.hip", """    auto advance = [&](int j) {
-        wait_vm<SCOPIES, true>();
+        wait_vm<SCOPIES + QLOADS, true>();
         __builtin_amdgcn_s_barrier();""", """    auto advance = [&](int j) {
         const unsigned long long ta = __builtin_amdgcn_s_memtime();
-        wait_vm<SCOPIES, true>();
+        wait_vm<SCOPIES + QLOADS, true>();
         const unsigned long long tb = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_barrier();
         const unsigned long long tcb = __builtin_amdgcn_s_memtime();
         sw += tb - ta; sb += tcb - tb;"""),
-    ("build.hip", "    Frags fa, fb;\n    issue(0);", "    const unsigned long long tl0 = __builtin_amdgcn_s_memtime(), tr0 = __builtin_amdgcn_s_memrealtime();\n    Frags fa, fb;\n    issue(0);"),
-    ("build.hip", "    // chunk j's copies landed (the chunk after it may fly)", "    unsigned long long sw = 0, sb = 0;\n    // chunk j's copies landed (the chunk after it may fly)"),
+    ("build.hip", "    TFrags fa, fb;\n", "    const unsigned long long tl0 = __builtin_amdgcn_s_memtime(), tr0 = __builtin_amdgcn_s_memrealtime();\n    TFrags fa, fb;\n"),
+    ("build.hip", "    // VMEM issue order per wave:", "    unsigned long long sw = 0, sb = 0;\n    // VMEM issue order per wave:"),
     ("build.hip", "    wait_vm<0, true>();             // the trailing zero chunks have landed and this wave's reads are done ...\n",
      "    wait_vm<0, true>();             // the trailing zero chunks have landed and this wave's reads are done ...\n"
      "    if (lane == 0 && blockIdx.x < 65536) { if (wave == 0) { g_stamps[blockIdx.x][0] = sw; g_stamps[blockIdx.x][1] = sb; "
@@ -136,7 +142,7 @@ PATCHES["prio"] = [("build.hip", "    // ---------------- epilogue (per wave, fr
                      "    // ---------------- epilogue (per wave, from registers) ----------------\n    __builtin_amdgcn_s_setprio(2);\n")]
 PATCHES["prio3"] = [("build.hip", "    // ---------------- epilogue (per wave, from registers) ----------------\n",
                      "    // ---------------- epilogue (per wave, from registers) ----------------\n    __builtin_amdgcn_s_setprio(3);\n")]
-COMBOS = {"stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
+COMBOS = {"stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
 
 
 def build(name):

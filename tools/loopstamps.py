@@ -21,9 +21,9 @@ with torch.no_grad():
         eraft_amd.CorrBlock(f1, f2)
     torch.cuda.synchronize()
 n = 11552
-buf = (ctypes.c_uint64 * (4 * n))()
+buf = (ctypes.c_uint64 * (5 * n))()   # ecorr_lab_stamps copies 5 words per block
 assert L.ecorr_lab_stamps(buf, n) == 0
-a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 4).astype(np.float64)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 5).astype(np.float64)
 for k, nm in enumerate(["wave0 dma wait", "wave0 barrier", "wave0 loop total", "loop realtime (10ns)"]):
     print(f"{nm:18s} cycles/block: median {np.median(a[:, k]):9.0f}  p10 {np.percentile(a[:, k], 10):9.0f}  p90 {np.percentile(a[:, k], 90):9.0f}")
 print(f"MFMA cycles per wave per tile (384 x 32): {384 * 32}")

@@ -76,3 +76,22 @@ print(f"per-CU time fractions (64 CUs): 2 blocks resident {busy2 / m:.2f}, epilo
 first = sorted(cus.items())[0]
 print("first CU timeline (us from kernel start): " +
       " ".join(f"[{us(t0[i] - base):.1f} {us(t1[i] - base):.1f} {us(t2[i] - base):.1f}]" for i in sorted(first[1], key=lambda i: t0[i])[:12]))
+
+# Loop progress rates by what the CU's other resident blocks are doing: per block, the time its K
+# loop spent beside another block's loop (tL), beside another's epilogue (tE) or alone (t0);
+# least squares for 1 loop = rL tL + rE tE + r0 t0 (rates in loops per us).
+rows = []
+for idx in cus.values():
+    for i in idx:
+        tl = te = 0.0
+        for j in idx:
+            if j == i:
+                continue
+            tl += max(0, min(t1[i], t1[j]) - max(t0[i], t0[j]))
+            te += max(0, min(t1[i], t2[j]) - max(t0[i], t1[j]))
+        tot = t1[i] - t0[i]
+        rows.append((us(tl), us(te), us(max(0, tot - tl - te))))
+A = np.array(rows)
+sol, *_ = np.linalg.lstsq(A, np.ones(len(A)), rcond=None)
+print("loop time split (median us): beside a loop {:.2f}, beside an epilogue {:.2f}, alone {:.2f}".format(*np.median(A, 0)))
+print("fitted loop time at each rate (us): beside a loop {:.2f}, beside an epilogue {:.2f}, alone {:.2f}".format(*(1 / sol)))
