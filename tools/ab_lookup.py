@@ -1,6 +1,12 @@
 #!/usr/bin/env python3
-"""Interleaved A/B timing of lookup variants (dev env knobs) in ONE process; outputs must be
-bitwise identical across variants."""
+"""Interleaved A/B of the radius-4 lookup between the tree's libecorr.so and AB_ALT_LIB lab builds
+(name=path,...) in ONE process, on one pyramid built by the tree library (DSEC B=16 60x80).
+Checks first that every library's lookup is bitwise identical to the tree's (AB_NOCHECK=1 skips:
+ablation builds), then times 12 lookups per round in rotated order.
+  AB_ALT_LIB=v=tools/v_lab/e-raft_amd/libecorr.so python tools/ab_lookup.py
+"""
+import ctypes
+import json
 import os
 import statistics
 import sys
@@ -9,17 +15,30 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tools"))
 import eraft_amd  # noqa: E402
+from eraft_amd import _lib  # noqa: E402
 
-VARIANTS = {"cols3reg": {}, "cols3": {"ECORR_LOOKUP_V": "3"}, "staged4": {"ECORR_LOOKUP_V": "4"}}
-if os.environ.get("AB_VARIANTS"):   # '{"name": {"KNOB": "v", ...}, ...}'
-    import json
-    VARIANTS = json.loads(os.environ["AB_VARIANTS"])
-KNOBS = ("ECORR_LOOKUP_QB", "ECORR_LOOKUP_V", "ECORR_LOOKUP_SKIP")
+
+def load(path):
+    L = ctypes.CDLL(path)
+    for name, (res, args) in _lib.SYMBOLS.items():
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+LIBS = {"tree": load(_lib.LIB_PATH)}
+for k, item in enumerate(filter(None, os.environ.get("AB_ALT_LIB", "").split(","))):
+    name, _, path = item.rpartition("=")
+    LIBS[name or f"alt{k}"] = load(os.path.join(ROOT, path))
 B, H, W, D = int(os.environ.get("AB_BATCH", "16")), 60, 80, 256
 g = torch.Generator(device="cuda").manual_seed(0)
 with torch.no_grad():
+    _lib._lib = LIBS["tree"]
     f1 = torch.randn((B, D, H, W), generator=g, device="cuda")
     f2 = torch.randn((B, D, H, W), generator=g, device="cuda")
     blk = eraft_amd.CorrBlock(f1, f2)
@@ -27,31 +46,31 @@ with torch.no_grad():
     init = torch.nn.functional.avg_pool2d(torch.randn((B, 2, H, W), generator=g, device="cuda") * 9.0, 5, 1, 2)
     coords = [(base + init + 0.5 * torch.randn((B, 2, H, W), generator=g, device="cuda")).contiguous()
               for _ in range(12)]
-    algo = B * H * W * 2904
-    times = {k: [] for k in VARIANTS}
-    ref = None
-    names = list(VARIANTS)
-    for rnd in range(int(os.environ.get("AB_ROUNDS", "6"))):
-        # rotate the order every round: the first variant of a round runs measurably slower
+    if not os.environ.get("AB_NOCHECK"):
+        ref = blk(coords[0])
+        for name, L in LIBS.items():
+            _lib._lib = L
+            same = torch.equal(blk(coords[0]), ref)
+            print(f"bitwise {name}: {'same' if same else 'DIFFERENT'}", flush=True)
+            if not same:
+                raise SystemExit(f"{name}: lookup differs")
+    times = {k: [] for k in LIBS}
+    names = list(LIBS)
+    for rnd in range(int(os.environ.get("AB_ROUNDS", "10"))):
         for name in names[rnd % len(names):] + names[:rnd % len(names)]:
-            env = VARIANTS[name]
-            for k in KNOBS:
-                os.environ.pop(k, None)
-            os.environ.update(env)
-            out = blk(coords[0])
-            torch.cuda.synchronize()
-            if ref is None:
-                ref = out.clone()
-            elif rnd == 0 and "skip" not in name:
-                assert torch.equal(out, ref), f"{name} output differs"
+            _lib._lib = LIBS[name]
+            for c in coords[:2]:
+                blk(c)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for c in coords:
                 blk(c)
             e1.record()
             torch.cuda.synchronize()
-            times[name].append(e0.elapsed_time(e1) / len(coords))
-for name, ts in times.items():
-    med = statistics.median(ts)
-    print(f"{name:8s} median {med * 1e3:.1f} us/call  min {min(ts) * 1e3:.1f}  -> {algo / med / 1e6:.0f} GB/s "
-          f"algorithmic ({algo / med / 1e6 / 8000 * 100:.1f}% of 8 TB/s)")
+            times[name].append(e0.elapsed_time(e1) / len(coords) * 1e3)
+    res = {}
+    for name, ts in times.items():
+        med = statistics.median(ts)
+        print(f"lookup B={B} {name:10s} median {med:.1f} us  min {min(ts):.1f}", flush=True)
+        res[name] = round(med, 1)
+    print(json.dumps({"ab_lookup_us": res}))

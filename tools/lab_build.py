@@ -112,8 +112,10 @@ PATCHES["stamps"] = [
 PATCHES["loopstamps"] = [
     ("build.hip", "constexpr int SQ = 256; ", STAMP_DECL + "__device__ unsigned long long g_lw, g_lb;\nconstexpr int SQ = 256; "),
     ("build.hip", """    auto advance = [&](int j) {
+        PHASE;
         wait_vm<SCOPIES + QLOADS, true>();
         __builtin_amdgcn_s_barrier();""", """    auto advance = [&](int j) {
+        PHASE;
         const unsigned long long ta = __builtin_amdgcn_s_memtime();
         wait_vm<SCOPIES + QLOADS, true>();
         const unsigned long long tb = __builtin_amdgcn_s_memtime();
@@ -142,7 +144,27 @@ PATCHES["prio"] = [("build.hip", "    // ---------------- epilogue (per wave, fr
                      "    // ---------------- epilogue (per wave, from registers) ----------------\n    __builtin_amdgcn_s_setprio(2);\n")]
 PATCHES["prio3"] = [("build.hip", "    // ---------------- epilogue (per wave, from registers) ----------------\n",
                      "    // ---------------- epilogue (per wave, from registers) ----------------\n    __builtin_amdgcn_s_setprio(3);\n")]
-COMBOS = {"stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
+# the K loop at issue priority 1, the epilogue back at 0: a block's MFMA stream ahead of the
+# co-resident block's epilogue VALU (which is older, so wins at equal priority)
+PATCHES["loopprio"] = [("build.hip", "    TFrags fa, fb;\n", "    __builtin_amdgcn_s_setprio(1);\n    TFrags fa, fb;\n"),
+                       ("build.hip", EPI, EPI + "    __builtin_amdgcn_s_setprio(0);\n")]
+PATCHES["loopprio3"] = [("build.hip", "    TFrags fa, fb;\n", "    __builtin_amdgcn_s_setprio(3);\n    TFrags fa, fb;\n"),
+                        ("build.hip", EPI, EPI + "    __builtin_amdgcn_s_setprio(0);\n")]
+# lookup ablations (timing only): no window loads / no output stores / no blends (one LDS read)
+PATCHES["lk_nostage"] = [("lookup_stage.h", "            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));",
+                          "            vals[c][ry] = (float)(need ? off : 0);")]
+PATCHES["lk_nostore"] = [("lookup.hip", """                const float v = blend(c[0], c[1], c[S], c[S + 1], wx[ai], wy[bb]);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
+                                                      sbase + (a * K + bb) * P.q_count * 4, 2);""",
+                          """                const float v = blend(c[0], c[1], c[S], c[S + 1], wx[ai], wy[bb]);
+                asm volatile("" :: "v"(v), "v"(sbase + (a * K + bb) * P.q_count * 4));""")]
+PATCHES["lk_noblend"] = [("lookup.hip", "                const float v = blend(c[0], c[1], c[S], c[S + 1], wx[ai], wy[bb]);",
+                          "                const float v = c[0];")]
+# lookup: every staging load issued twice (same bytes, 2x the lane requests): is staging bound by
+# the per-lane request rate?
+PATCHES["lk_dbl"] = [("lookup_stage.h", "            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));",
+                      "            vals[c][ry] = __builtin_fmaf(0.0f, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 1)), __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0)));")]
+COMBOS = {"loopstamps_epioob": ["loopstamps", "epioob"], "stamps_loopprio": ["stamps", "loopprio"], "stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
 
 
 def build(name):
