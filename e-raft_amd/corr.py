@@ -15,6 +15,17 @@ Contract differences, all loud: inputs must be fp32 HIP tensors (the reference p
 eraft.py:104-105); the block is forward-only (E-RAFT only ever calls it under torch.no_grad(),
 test.py:80) and refuses inputs that require grad while grad mode is on; coords must match the
 build's (B, 2, H, W) exactly.
+
+Numerics: the default build sums each product as f16 lo*hi + hi*lo + hi*hi of per-pixel-scaled
+operands: within 1e-5 normwise of the reference and closer to fp64 than its fp32
+GEMM, pooling and lookup bit-exact given level 0.  One semantic difference: an fmap pixel holding
++-inf yields NaN (not +-inf) in its level-0 row/column, because the lo half of an infinite value
+is NaN; NaN inputs give NaN in both.  ECORR_BUILD_MODE=fp32 (read once at import) selects the
+fp32-MFMA build, which keeps the reference's inf semantics.
+
+corr_pyramid is a materialized COPY in the reference layout: 4 levels of B*H*W query images
+(1.96 GB at DSEC B=16, the whole pyramid again), made on first access and cached on the block.
+Nothing on the E-RAFT path reads it; access it only for inspection or tests.
 """
 import torch
 

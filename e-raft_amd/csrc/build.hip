@@ -114,8 +114,7 @@ __device__ __forceinline__ float* level_px(const BuildParams& P, int L, int64_t 
 // ============================================================================================
 // Split GEMM (default).  Block tile: 256 queries (two 128-query fmap1 panels) x one 128-target
 // n-tile (one fmap2 panel); 4 waves, wave w = queries 64 w .. 64 w + 63 x all 128 targets = 2 x 4
-// v_mfma_f32_32x32x16_f16 tiles (128 accumulators, pinned to AGPRs), so every K chunk reads 12
-// fragments for 24 MFMAs (0.5 KB of LDS per MFMA, 0.67 in round 1).  Two blocks per CU.
+// v_mfma_f32_32x32x16_f16 tiles (128 accumulators, pinned to AGPRs).  Two blocks per CU.
 //
 // The MFMAs take the fmap2 fragment as their A operand: the accumulators hold C^T, lane (acol,
 // arow) of tile (i, j) owns query 32 i + acol and targets 32 j + 8 g4 + 4 arow + t (reg 4 g4 + t).
@@ -125,23 +124,21 @@ __device__ __forceinline__ float* level_px(const BuildParams& P, int L, int64_t 
 // the 8 x 8 pool needs one value from lane acol + 32.  Band tiles (4 x 32): rows g4, cols 8 j +
 // 4 arow + t.
 //
-// K loop: each 16-deep chunk's three panels (24 KB) go global -> LDS verbatim by LDS-DMA
-// (buffer_load_dwordx4 ... lds, 6 per wave) through 3 buffers, one chunk in flight behind the one
-// being read; one barrier per chunk; fragments are lane-linear ds_read_b128 (conflict-free).
-// Chunk kc + 1's barrier and first fragments are read between chunk kc's lo*hi MFMAs and its
-// hi*lo / hi*hi MFMAs.  Chunks past the end are issued as out-of-range loads (they land as
-// zeros), which keeps every wait count static.
+// K loop: the target panel (shared by the 4 waves) goes global -> LDS verbatim by LDS-DMA
+// (buffer_load_dwordx4 ... lds, 2 per wave and chunk) through 3 buffers, two chunks ahead; the
+// query fragments (wave-private) go global -> VGPR, two chunks ahead.  One barrier per chunk;
+// target fragments are lane-linear ds_read_b128 (conflict-free).  Chunk kc + 1's barrier and
+// first fragments are read between chunk kc's lo*hi MFMAs and its hi*lo / hi*hi MFMAs.  Chunks
+// past the end are issued as out-of-range loads (they land as zeros), which keeps every wait
+// count static.
 //
-// Epilogue, straight from the accumulators (no LDS, no barrier): scale by 2^-(e_q + e_t) /
-// sqrt(D), pool 8x8 -> 4x4 -> 2x2 -> 1 in registers in the reference's order, then store.  Store
-// shape matters more than anything else here (tools/store_lab.hip, DSEC level-0 shape): 32-byte
-// pieces per query per instruction run at 5.2 TB/s only as plain stores, which keep every line
-// in L2 and evict the operand panels (PMC: 1 GB of panel re-reads per build instead of 0.33 GB);
-// 64-byte pieces run at 5.3-5.5 TB/s with sc1 stores, which leave L2 right away.  So levels 0
-// and 1 are assembled into 64-byte line segments in registers -- v_permlane32_swap gives lane
-// acol rows 0-1 and lane acol + 32 rows 2-3 of a line, a DPP transpose over each 4-lane quad
-// gives 4 adjacent lanes the 4 pieces of one query's segment -- and every store instruction
-// writes 8 whole 128-byte lines.  Levels 2-3 (6% of the bytes) are single pixels, plain stores.
+// Epilogue, per wave from its accumulators: scale by 2^-(e_q + e_t) / sqrt(D), pool 8x8 -> 4x4 ->
+// 2x2 -> 1 in registers in the reference's order, then store.  Store shape matters more than
+// anything else here (tools/store_lab.hip, DSEC level-0 shape): whole 128-byte lines run at
+// 5.2-5.5 TB/s with any cache policy; 32-byte pieces only as plain stores, which keep every line
+// in L2 and evict the operand panels (PMC: 1 GB of panel re-reads per build).  So level-0 and
+// level-1 lines pass through a wave-private LDS transpose and leave whole with nt sc1 (write
+// through, out of L2); levels 2-3 (6% of the bytes) leave as 16- / 8-byte row pieces.
 // ============================================================================================
 constexpr int SQ = 256;                     // queries per split tile
 constexpr int SCHUNK = PANEL;               // LDS bytes per K chunk (the target panel)
