@@ -11,14 +11,19 @@ One step = one pass of the hot path over one batch: CorrBlock build (split-f16 o
       batch of pairs, no data-path collective ("weak" scaling).
   --mode rowshard: BASELINE configs[4] -- 1280x720 (fmap 256 x 92 x 160, padded 736 rows), batch
       4, query rows sharded over the N ranks, fmap2 row slabs all-gathered once per pair and the
-      lookup output slabs once per iteration over RCCL ("strong" scaling).
+      lookup output slabs once per iteration (one fixed-chunk all-gather each, RCCL; "strong"
+      scaling).
 
     python bench.py [--gpus N --steps K --warmup W --batch 16 --no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 
-Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP-event timed over the timed
-region on the launch stream) and `cpu_baseline` (the torch-CPU restatement of the reference,
-oracle/torch_ref.py, timed on this host's cores on a bounded sample, rank 0 at N=1 only).
+Prints ONE JSON line on rank 0 with `roofline` (the dominant kernel, build_split_kernel alone,
+HIP events on its launch stream inside the timed region; `window_frac` = the whole build with its
+operand pass; `traffic` = PMC HBM bytes from profiles/latest_pmc.json when its source digest
+matches this tree), `kernels` (build, pack, lookup, build_fp32) and `cpu_baseline` (SURVEY 8(d):
+the C1 shape, B = 1, build + 12 lookups on the GPU leg's first pair; the torch restatement of the
+reference's ATen ops, oracle/torch_ref.py, on all host cores and on one core, and the C oracle;
+median of 3 after a warm-up; rank 0 at N=1 only).
 BENCH_SINGLE_DEVICE=1 puts every rank on cuda:0 with gloo (multi-process rehearsal on one GPU).
 """
 import argparse
