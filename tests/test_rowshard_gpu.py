@@ -99,3 +99,42 @@ def test_rowshard_two_ranks_bit_exact(shape):
         bad = [k for k, v in r.items() if not v]
         assert not bad, f"rank {rank}: {bad}"
     assert all(len(r[1]) == 8 for r in res)
+
+
+def _rccl_worker(port, q):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        import prng
+        from eraft_amd.rowshard import RowExchange
+        B, C, H, W = 2, 324, 23, 40
+        full = torch.from_numpy(prng.normal(81, (B, C, H, W))).cuda()
+        ex = RowExchange(H)
+        ok = []
+        for it in range(2):   # persistent buffers
+            ex.send_slab(B, C, W, device=full.device).copy_(full + it)
+            ok.append(bool(torch.equal(ex.gather(B, C, W, full.device), full + it)))
+        q.put((all(ok), dist.get_backend(), None))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((False, None, repr(e)))
+
+
+def test_row_exchange_over_rccl_one_rank():
+    """The RCCL branch of the exchange (all_gather_into_tensor into the persistent receive buffer,
+    then ecorr_rows_assemble) on the one GPU this box has: a 1-rank "nccl" group.  Multi-rank RCCL
+    runs only on multi-GPU nodes (the driver's scaling bench)."""
+    if not torch.cuda.is_available():
+        pytest.fail("no HIP device visible")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    ok, backend, err = q.get(timeout=180)
+    p.join(timeout=60)
+    assert err is None, err
+    assert backend == "nccl" and ok
