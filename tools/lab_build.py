@@ -164,6 +164,30 @@ PATCHES["lk_noblend"] = [("lookup.hip", "                const float v = blend(c
 # the per-lane request rate?
 PATCHES["lk_dbl"] = [("lookup_stage.h", "            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));",
                       "            vals[c][ry] = __builtin_fmaf(0.0f, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 1)), __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0)));")]
+# lookup: output stores as 2 x dwordx4 + 1 dword per column (same bytes, 3 store instructions
+# instead of 9; wrong layout -- timing only): does the store request count bound the lookup?
+PATCHES["lk_st4"] = [("lookup.hip", """#pragma unroll
+            for (int bb = 0; bb < K; ++bb) {
+                const float* c = wc + yo[bb];
+                const float v = blend(c[0], c[1], c[S], c[S + 1], wx[ai], wy[bb]);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
+                                                      sbase + (a * K + bb) * P.q_count * 4, 2);
+            }""", """            float vv[K];
+#pragma unroll
+            for (int bb = 0; bb < K; ++bb) {
+                const float* c = wc + yo[bb];
+                vv[bb] = blend(c[0], c[1], c[S], c[S + 1], wx[ai], wy[bb]);
+            }
+            if constexpr (K == 9) {
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, floatx4_t{vv[0], vv[1], vv[2], vv[3]}), orsrc, voff * 4, sbase + (a * K) * P.q_count * 4, 2);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, floatx4_t{vv[4], vv[5], vv[6], vv[7]}), orsrc, voff * 4, sbase + (a * K + 4) * P.q_count * 4, 2);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vv[8]), orsrc, voff, sbase + (a * K + 8) * P.q_count * 4, 2);
+            }"""),
+                     ("lookup.hip", "constexpr int NT = 256;   // threads of the generic kernels",
+                      "constexpr int NT = 256;   // threads of the generic kernels\ntypedef float floatx4_t __attribute__((ext_vector_type(4)));")]
+# tile order: m-tiles per group of the grouped order (tree: 8)
+for _gm in (2, 3, 4, 6):
+    PATCHES[f"gm{_gm}"] = [("build.hip", "    constexpr int GM = 8;", f"    constexpr int GM = {_gm};")]
 COMBOS = {"loopstamps_epioob": ["loopstamps", "epioob"], "stamps_loopprio": ["stamps", "loopprio"], "stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
 
 
