@@ -188,7 +188,19 @@ PATCHES["lk_st4"] = [("lookup.hip", """#pragma unroll
 # tile order: m-tiles per group of the grouped order (tree: 8)
 for _gm in (2, 3, 4, 6):
     PATCHES[f"gm{_gm}"] = [("build.hip", "    constexpr int GM = 8;", f"    constexpr int GM = {_gm};")]
+# timing only: each v_mfma_f32_32x32x16_f16 replaced by two v_mfma_f32_16x16x32_f16 on the same
+# fragments (the same MAC count, garbage sums): does the 16x16 shape hold a higher clock here?
+def _m16(x, y):
+    return ("build.hip", f"acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16({x}, {y}, acc[i][j], 0, 0, 0);",
+            "{ floatx4 c0 = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]}, "
+            "c1 = {acc[i][j][4], acc[i][j][5], acc[i][j][6], acc[i][j][7]}; "
+            f"c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16({x}, {y}, c0, 0, 0, 0); "
+            f"c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16({x}, {y}, c1, 0, 0, 0); "
+            "acc[i][j][0] = c0[0]; acc[i][j][1] = c0[1]; acc[i][j][2] = c0[2]; acc[i][j][3] = c0[3]; "
+            "acc[i][j][4] = c1[0]; acc[i][j][5] = c1[1]; acc[i][j][6] = c1[2]; acc[i][j][7] = c1[3]; }")
+PATCHES["mfma16"] = [_m16("f.th[j]", "q.ql[i]"), _m16("f.tl[j]", "q.qh[i]"), _m16("f.th[j]", "q.qh[i]")]
 COMBOS = {"loopstamps_epioob": ["loopstamps", "epioob"], "stamps_loopprio": ["stamps", "loopprio"], "stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
+COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"], "loopstamps_noepi_mfma16": ["loopstamps", "noepi", "mfma16"]})
 
 
 def build(name):
