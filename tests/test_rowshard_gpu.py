@@ -138,3 +138,29 @@ def test_row_exchange_over_rccl_one_rank():
     p.join(timeout=60)
     assert err is None, err
     assert backend == "nccl" and ok
+
+
+@pytest.mark.parametrize("world,B,C,H,W", [(3, 2, 5, 7, 9), (8, 4, 324, 92, 160), (2, 1, 3, 5, 8), (4, 2, 7, 4, 13)])
+def test_rows_assemble_kernel(world, B, C, H, W):
+    """ecorr_rows_assemble alone on chunk data of the all-gather layout (16-byte and scalar paths,
+    ragged partitions), against a test-side reassembly."""
+    if not torch.cuda.is_available():
+        pytest.fail("no HIP device visible")
+    import eraft_amd
+    from eraft_amd import _lib
+    from eraft_amd.rowshard import row_partition
+    starts, counts = row_partition(H, world)
+    chunk = B * C * max(counts) * W
+    recv = torch.randn(world * chunk, device="cuda")
+    out = torch.full((B, C, H, W), float("nan"), device="cuda")
+    eraft_amd.lib()
+    _lib.check(_lib.lib().ecorr_rows_assemble(recv.data_ptr(), chunk, world, B, C, H, W, out.data_ptr(),
+                                              _lib.stream_of(out)), "rows assemble")
+    ref = torch.empty_like(out)
+    ch = recv.view(world, chunk)
+    for r in range(world):
+        ref[:, :, starts[r]:starts[r] + counts[r]] = ch[r, :B * C * counts[r] * W].view(B, C, counts[r], W)
+    assert torch.equal(out, ref)
+    # loud on a chunk too small for the partition
+    assert _lib.lib().ecorr_rows_assemble(recv.data_ptr(), chunk - 1, world, B, C, H, W, out.data_ptr(),
+                                          _lib.stream_of(out)) != 0

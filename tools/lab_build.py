@@ -199,6 +199,9 @@ def _m16(x, y):
             "acc[i][j][0] = c0[0]; acc[i][j][1] = c0[1]; acc[i][j][2] = c0[2]; acc[i][j][3] = c0[3]; "
             "acc[i][j][4] = c1[0]; acc[i][j][5] = c1[1]; acc[i][j][6] = c1[2]; acc[i][j][7] = c1[3]; }")
 PATCHES["mfma16"] = [_m16("f.th[j]", "q.ql[i]"), _m16("f.tl[j]", "q.qh[i]"), _m16("f.th[j]", "q.qh[i]")]
+# lookup: unneeded window elements skipped by exec mask instead of an out-of-range offset
+PATCHES["lk_exec"] = [("lookup_stage.h", "            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));",
+                       "            vals[c][ry] = need ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0)) : 0.0f;")]
 COMBOS = {"loopstamps_epioob": ["loopstamps", "epioob"], "stamps_loopprio": ["stamps", "loopprio"], "stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"], "loopstamps_noepi_mfma16": ["loopstamps", "noepi", "mfma16"]})
 
