@@ -137,8 +137,8 @@ __device__ __forceinline__ float* level_px(const BuildParams& P, int L, int64_t 
 // anything else here (tools/store_lab.hip, DSEC level-0 shape): whole 128-byte lines run at
 // 5.2-5.5 TB/s with any cache policy; 32-byte pieces only as plain stores, which keep every line
 // in L2 and evict the operand panels (PMC: 1 GB of panel re-reads per build).  So level-0 and
-// level-1 lines pass through a wave-private LDS transpose and leave whole with nt sc1 (write
-// through, out of L2); levels 2-3 (6% of the bytes) leave as 16- / 8-byte row pieces.
+// level-1 lines pass through a wave-private LDS transpose and leave whole as non-temporal stores
+// (out of L2); levels 2-3 (6% of the bytes) leave as 16- / 8-byte row pieces.
 // ============================================================================================
 constexpr int SQ = 256;                     // queries per split tile
 constexpr int SCHUNK = PANEL;               // LDS bytes per K chunk (the target panel)
@@ -147,7 +147,8 @@ constexpr int SCOPIES = SCHUNK / 1024 / 4;  // LDS-DMA copies per wave per chunk
 constexpr int QLOADS = 4;                   // query fragment loads per wave per chunk (hi, lo x 2 rows)
 constexpr int SLDS = 4 * 4 * 32 * 144;      // LDS bytes: the epilogue's transpose regions (> the K loop's)
 constexpr int SOOB = 0x7ffffff0;            // buffer offset beyond any panel: loads 0, touches nothing
-constexpr int ST_SC1 = 18;                  // level-0/1 store cache policy: nt sc1 (write through, drop from L2)
+constexpr int ST_L01 = 2;                   // level-0/1 store cache policy: nt (A/B: 725 vs 731 us for nt sc1;
+                                            // plain and sc1 alone ~1000 us: the lines stay in L2 and evict the panels)
 constexpr int XS = 144;                     // LDS bytes per query of the epilogue's line transpose
 static_assert(4 * 4 * 32 * XS <= SLDS && SNBUF * SCHUNK <= SLDS, "LDS regions");
 
@@ -384,7 +385,7 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
 #pragma unroll
         for (int s = 0; s < 4; ++s)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, pc[s]), rs,
-                                                   ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_SC1);
+                                                   ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_L01);
     };
     // N adjacent pixels (r, c .. c + N - 1) of level 2 or 3 (tiled: inside one tile row; compact:
     // row-major), plain stores; pixels outside the level are dropped

@@ -39,6 +39,7 @@ PATCHES = {
     # store cache policy of the level-0/1 segments: sc1, plain (tree: nt sc1)
     "stsc1": [("build.hip", "constexpr int ST_SC1 = 18;", "constexpr int ST_SC1 = 16;")],
     "stplain": [("build.hip", "constexpr int ST_SC1 = 18;", "constexpr int ST_SC1 = 0;")],
+    "stnt": [("build.hip", "constexpr int ST_SC1 = 18;", "constexpr int ST_SC1 = 2;")],
     # the second wave of resident blocks starts ~12 us late (do co-resident blocks run in phase?)
     "stagger": [("build.hip", "    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n    const int acol",
                  "    if (blockIdx.x >= 256 && blockIdx.x < 512)\n        for (int z = 0; z < 3; ++z) __builtin_amdgcn_s_sleep(127);\n"
@@ -202,7 +203,17 @@ PATCHES["mfma16"] = [_m16("f.th[j]", "q.ql[i]"), _m16("f.tl[j]", "q.qh[i]"), _m1
 # lookup: unneeded window elements skipped by exec mask instead of an out-of-range offset
 PATCHES["lk_exec"] = [("lookup_stage.h", "            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));",
                        "            vals[c][ry] = need ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0)) : 0.0f;")]
+# epilogue ablations (timing only): no scaling (raw accumulators), no LDS transposes (the
+# read-back replaced by the lane's own registers)
+PATCHES["epi_noscale"] = [("build.hip", "const float x = __fmul_rn(acc[i][j][4 * g4 + t], __fmul_rn(sq, s4[t]));",
+                           "const float x = acc[i][j][4 * g4 + t]; (void)s4; (void)sq;")]
+PATCHES["epi_nolds"] = [("build.hip", "        for (int s = 0; s < 4; ++s) pc[s] = *reinterpret_cast<const floatx4*>(xp + ro + s * XS);",
+                         "        for (int s = 0; s < 4; ++s) pc[s] = floatx4{(float)(ro + s), (float)ql, (float)lo, 1.0f};"),
+                        ("build.hip", """                    *reinterpret_cast<floatx4*>(xp + wo + 32 * g4 + 16 * arow) =
+                        floatx4{v[jl][g4][0], v[jl][g4][1], v[jl][g4][2], v[jl][g4][3]};""",
+                         """                    asm volatile("" :: "v"(floatx4{v[jl][g4][0], v[jl][g4][1], v[jl][g4][2], v[jl][g4][3]}));""")]
 COMBOS = {"loopstamps_epioob": ["loopstamps", "epioob"], "stamps_loopprio": ["stamps", "loopprio"], "stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
+COMBOS.update({"stamps_epi_noscale": ["stamps", "epi_noscale"], "stamps_epi_nolds": ["stamps", "epi_nolds"]})
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"], "loopstamps_noepi_mfma16": ["loopstamps", "noepi", "mfma16"]})
 
 
