@@ -212,7 +212,43 @@ PATCHES["epi_nolds"] = [("build.hip", "        for (int s = 0; s < 4; ++s) pc[s]
                         ("build.hip", """                    *reinterpret_cast<floatx4*>(xp + wo + 32 * g4 + 16 * arow) =
                         floatx4{v[jl][g4][0], v[jl][g4][1], v[jl][g4][2], v[jl][g4][3]};""",
                          """                    asm volatile("" :: "v"(floatx4{v[jl][g4][0], v[jl][g4][1], v[jl][g4][2], v[jl][g4][3]}));""")]
+# on top of loopstamps: the wait for the chunk's query fragments made explicit and timed before
+# each lo*hi MFMA group (g_stamps[block][4] = wave 0's cycles in those waits)
+PATCHES["qwait"] = [("build.hip", "        mfma_lohi(fa, qa);", "        { const unsigned long long t0 = __builtin_amdgcn_s_memtime(); wait_vm<6, false>(); sq += __builtin_amdgcn_s_memtime() - t0; }\n        mfma_lohi(fa, qa);"),
+                    ("build.hip", "        mfma_lohi(fb, qb);", "        { const unsigned long long t0 = __builtin_amdgcn_s_memtime(); wait_vm<6, false>(); sq += __builtin_amdgcn_s_memtime() - t0; }\n        mfma_lohi(fb, qb);"),
+                    ("build.hip", "    unsigned long long sw = 0, sb = 0;", "    unsigned long long sw = 0, sb = 0, sq = 0;"),
+                    ("build.hip", "g_stamps[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime() - tr0; }", "g_stamps[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime() - tr0; if (wave == 0) g_stamps[blockIdx.x][4] = sq; }")]
+# stamps for the S16 loop (stamp 1 after split_loop16; build.hip with tools/lab_patches/s16_loop.diff applied)
+PATCHES["stamps16"] = [x for x in PATCHES["stamps"] if "chunk buffers are the epilogue" not in x[1]] + [
+    ("build.hip", "        split_loop16(P, smem, rq, rt, pstride, wave, lane, acc);\n",
+     "        split_loop16(P, smem, rq, rt, pstride, wave, lane, acc);\n        stamp(1);\n")]
+# in-loop clock and wait/barrier cycles of the S16 loop -> g_stamps[block] = {wait, barrier, total, realtime}
+PATCHES["loopstamps16"] = [
+    ("build.hip", "constexpr int SQ = 256; ", STAMP_DECL + "constexpr int SQ = 256; "),
+    ("build.hip", """    QH qa, qb;
+    issue(0);""", """    QH qa, qb;
+    unsigned long long sw = 0, sb = 0;
+    const unsigned long long tl0 = __builtin_amdgcn_s_memtime(), tr0 = __builtin_amdgcn_s_memrealtime();
+    issue(0);"""),
+    ("build.hip", """        if (step == 0) wait_vm<6, true>();
+        else wait_vm<12, true>();
+        __builtin_amdgcn_s_barrier();""", """        const unsigned long long ta = __builtin_amdgcn_s_memtime();
+        if (step == 0) wait_vm<6, true>();
+        else wait_vm<12, true>();
+        const unsigned long long tb = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_barrier();
+        sw += tb - ta; sb += __builtin_amdgcn_s_memtime() - tb;"""),
+    ("build.hip", """#undef PHASE
+    wait_vm<0, true>();
+    __builtin_amdgcn_s_barrier();   // every wave is done with the ring""", """#undef PHASE
+    wait_vm<0, true>();
+    if (lane == 0 && wave == 0 && blockIdx.x < 65536) { g_stamps[blockIdx.x][0] = sw; g_stamps[blockIdx.x][1] = sb;
+        g_stamps[blockIdx.x][2] = __builtin_amdgcn_s_memtime() - tl0; g_stamps[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime() - tr0; }
+    __builtin_amdgcn_s_barrier();   // every wave is done with the ring"""),
+    ("build.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + STAMP_EXPORT),
+]
 COMBOS = {"loopstamps_epioob": ["loopstamps", "epioob"], "stamps_loopprio": ["stamps", "loopprio"], "stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
+COMBOS.update({"loopstamps_qwait": ["loopstamps", "qwait"]})
 COMBOS.update({"stamps_epi_noscale": ["stamps", "epi_noscale"], "stamps_epi_nolds": ["stamps", "epi_nolds"]})
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"], "loopstamps_noepi_mfma16": ["loopstamps", "noepi", "mfma16"]})
 

@@ -24,7 +24,7 @@ n = 11552
 buf = (ctypes.c_uint64 * (5 * n))()   # ecorr_lab_stamps copies 5 words per block
 assert L.ecorr_lab_stamps(buf, n) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 5).astype(np.float64)
-for k, nm in enumerate(["wave0 dma wait", "wave0 barrier", "wave0 loop total", "loop realtime (10ns)"]):
+for k, nm in enumerate(["wave0 dma wait", "wave0 barrier", "wave0 loop total", "loop realtime (10ns)", "wave0 q wait (qwait)"]):
     print(f"{nm:18s} cycles/block: median {np.median(a[:, k]):9.0f}  p10 {np.percentile(a[:, k], 10):9.0f}  p90 {np.percentile(a[:, k], 90):9.0f}")
 print(f"MFMA cycles per wave per tile (384 x 32): {384 * 32}")
 print(f"in-loop clock: {np.median(a[:, 2] / (a[:, 3] * 10e-9)) / 1e9:.3f} GHz (s_memtime / s_memrealtime)")
