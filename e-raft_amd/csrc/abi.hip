@@ -25,7 +25,15 @@ int pyramid_geometry(int64_t rows, int H, int W, int levels, PyrGeom* g) {
         if (hh == 0 || ww == 0) return ECORR_ESHAPE;
         g->h[i] = hh;
         g->w[i] = ww;
-        if (level_compact(i, hh, ww)) {
+        int64_t nrows = rows;
+        if (i == 2 || i == 3) {   // interleaved (ecorr_device.h pix_off): blocks of (8 >> i) x (16 >> i)
+            const int bh = 1 << ilv_sy(i), bw = 1 << ilv_sx(i);
+            const int nby = (hh + bh - 1) / bh, nbx = (ww + bw - 1) / bw;
+            g->ntx[i] = -nbx;
+            g->nty[i] = nby;
+            g->sz[i] = (int64_t)nby * nbx * bh * bw;
+            nrows = (rows + kGroup - 1) / kGroup * kGroup;
+        } else if (level_compact(i, hh, ww)) {
             g->ntx[i] = 0;
             g->nty[i] = hh;
             g->sz[i] = (int64_t)hh * ww;
@@ -35,7 +43,7 @@ int pyramid_geometry(int64_t rows, int H, int W, int levels, PyrGeom* g) {
             g->sz[i] = (int64_t)pad_h(hh) * pad_w(ww);
         }
         g->off[i] = o;
-        o += rows * g->sz[i];
+        o += nrows * g->sz[i];
         o = (o + kTile - 1) & ~(int64_t)(kTile - 1);   // every level starts on a 128-byte line
     }
     g->off[levels] = o;

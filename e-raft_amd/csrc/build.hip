@@ -51,11 +51,12 @@ __device__ __forceinline__ float pool4_v(float a, float b, float c, float d) {
 // 2^e as a float, e in [-126, 127]
 __device__ __forceinline__ float exp2i(int e) { return __int_as_float((e + 127) << 23); }
 
-// s_waitcnt vmcnt(N) with lgkmcnt(0) (LGKM0) or left alone; expcnt never waited (N < 16)
+// s_waitcnt vmcnt(N) with lgkmcnt(0) (LGKM0) or left alone; expcnt never waited (gfx9 encoding:
+// vmcnt bits 3:0 and 15:14)
 template <int N, bool LGKM0>
 __device__ __forceinline__ void wait_vm() {
-    static_assert(N >= 0 && N < 16, "vmcnt field");
-    __builtin_amdgcn_s_waitcnt(N | (7 << 4) | (LGKM0 ? 0 : (15 << 8)));
+    static_assert(N >= 0 && N < 64, "vmcnt field");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (LGKM0 ? 0 : (15 << 8)));
 }
 
 // Bijective XCD-aware remap (cdna_hip_programming.md §5 T1): consecutive logical tiles land on
@@ -100,8 +101,13 @@ __device__ __forceinline__ void decode_tile(const BuildParams& P, int t, int n_m
 }
 
 // One pooled-level pixel (row, col) of a query image: tiled (ntx > 0; the tile must exist, cells
-// in a tile's padding are written and never read) or compact row-major (range-checked).
+// in a tile's padding are written and never read), interleaved (ntx < 0; likewise the block) or
+// compact row-major (range-checked).
 __device__ __forceinline__ float* level_px(const BuildParams& P, int L, int64_t row_img, int r, int c) {
+    if (P.lntx[L] < 0) {   // interleaved (levels 2, 3): the block must exist
+        if ((r >> ilv_sy(L)) >= P.lnty[L] || (c >> ilv_sx(L)) >= -P.lntx[L]) return nullptr;
+        return P.lvl[L] + pix_off(row_img, r, c, L, P.lntx[L], P.lw[L], P.lsz[L]);
+    }
     float* img = P.lvl[L] + row_img * P.lsz[L];
     if (P.lntx[L] > 0) {
         if ((r >> 2) >= P.lnty[L] || (c >> 3) >= P.lntx[L]) return nullptr;
@@ -308,6 +314,57 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
         PHASE;
     };
 
+    if constexpr (NK > 0) {
+        // D known at compile time: query fragments two chunks ahead in three register sets.  VMEM
+        // issue order per wave t(0) q(0) t(1) q(1) | t(2) q(2) | t(3) q(3) ...: chunk c issues
+        // t(c + 3) in advance(c + 1) and q(c + 3) at its end, so at advance(j)'s wait the 10 younger
+        // q(j), t(j + 1), q(j + 1) may fly.
+        TFrags f[2];
+        QFrags qs[3];
+        // (no query loads past the last chunk: hipcc deletes loads whose registers are never read,
+        // so the waits count only the loads that exist)
+        auto advance3 = [&](int j) {
+            PHASE;
+            if (j + 1 < NK) wait_vm<QLOADS + SCOPIES + QLOADS, true>();
+            else if (j < NK) wait_vm<QLOADS + SCOPIES, true>();
+            else wait_vm<SCOPIES, true>();
+            __builtin_amdgcn_s_barrier();
+            PHASE;
+            issue(j + 2);
+            PHASE;
+        };
+        issue(0);
+        PHASE;
+        load_q(0, qs[0]);
+        PHASE;
+        issue(1);
+        PHASE;
+        load_q(1, qs[1]);
+        PHASE;
+        wait_vm<QLOADS + SCOPIES + QLOADS, true>();   // t(0) landed
+        __builtin_amdgcn_s_barrier();
+        PHASE;
+        issue(2);
+        PHASE;
+        read_lo(0, f[0]);
+        read_hi(0, f[0]);
+        PHASE;
+        load_q(2, qs[2]);
+        PHASE;
+#pragma unroll
+        for (int kc = 0; kc < NK; ++kc) {
+            mfma_lohi(f[kc & 1], qs[kc % 3]);
+            PHASE;
+            advance3(kc + 1);
+            read_lo(kc + 1, f[(kc + 1) & 1]);
+            PHASE;
+            mfma_rest(f[kc & 1], qs[kc % 3]);
+            PHASE;
+            read_hi(kc + 1, f[(kc + 1) & 1]);
+            if (kc + 3 < NK) load_q(kc + 3, qs[kc % 3]);
+            PHASE;
+        }
+    } else {
     TFrags fa, fb;
     QFrags qa, qb;
     issue(0);
@@ -350,6 +407,7 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
         load_q(kc + 3, qb);
         PHASE;
     }
+    }
 #undef PHASE
     wait_vm<0, true>();             // the trailing zero chunks have landed and this wave's reads are done ...
     __builtin_amdgcn_s_barrier();   // ... in every wave: the chunk buffers are the epilogue's scratch
@@ -372,8 +430,14 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
     const int L = P.fused_levels;
     const int64_t rows0 = (int64_t)b * P.q_count + q0;   // the block's first query image
     const int nq = min(SQ, P.q_count - q0);
-    // per-level descriptors over the block's query images (range check = query bound)
+    // per-level descriptors over the block's query images (range check = query bound); levels 2-3
+    // (interleaved): over the 64-row groups the block's rows touch, from group g0 = rows0 / 64
+    const int64_t g0 = rows0 >> 6;
     auto rsrc_of = [&](int lv) {
+        if (lv >= 2)
+            return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + g0 * kGroup * P.lsz[lv], 0,
+                                                     (int)((((rows0 + nq - 1) >> 6) - g0 + 1) * kGroup * P.lsz[lv] * 4),
+                                                     0x00020000);
         return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + rows0 * P.lsz[lv], 0, (int)(nq * P.lsz[lv] * 4), 0x00020000);
     };
     // read the transposed segments back and store them: line byte offset lo (+ the query image)
@@ -387,24 +451,23 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, pc[s]), rs,
                                                    ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_L01);
     };
-    // N adjacent pixels (r, c .. c + N - 1) of level 2 or 3 (tiled: inside one tile row; compact:
-    // row-major), plain stores; pixels outside the level are dropped
+    // One block row (r, c .. c + N - 1), N = the block width, of level 2 or 3 (interleaved) for
+    // block-local query qloc: lanes on consecutive queries write consecutive 4N-byte pieces, so a
+    // store instruction covers whole lines.  Queries past the block and blocks outside the level
+    // are dropped (padding cells of a block are written and never read).
     auto store_px = [&](__amdgpu_buffer_rsrc_t rs, int lv, int qloc, int r, int c, auto val) {
         constexpr int N = sizeof(val) / 4;
-        const bool tiled = P.lntx[lv] > 0;
-        const int off = (int)((qloc * P.lsz[lv] + level_off(r, c, P.lntx[lv], P.lw[lv])) * 4);
-        if (tiled || c + N <= P.lw[lv]) {   // whole vector in (tiled: padding cells absorb the rest)
-            const bool in = tiled ? ((r >> 2) < P.lnty[lv] && (c >> 3) < P.lntx[lv]) : r < P.lh[lv];
-            if constexpr (N == 4)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, 0);
-            else
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, val), rs, in ? off : SOOB, 0, 0);
-        } else {   // compact level, ragged right edge
-#pragma unroll
-            for (int k = 0; k < N; ++k)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val[k]), rs,
-                                                      r < P.lh[lv] && c + k < P.lw[lv] ? off + 4 * k : SOOB, 0, 0);
-        }
+        const int sy = ilv_sy(lv), sx = ilv_sx(lv);
+        const int by = r >> sy, bx = c >> sx;
+        const bool in = qloc < nq && by < P.lnty[lv] && bx < -P.lntx[lv];
+        const int64_t R = rows0 + qloc;
+        const int off = (int)((((R >> 6) - g0) * kGroup * P.lsz[lv] +
+                               ((int64_t)(by * -P.lntx[lv] + bx) * kGroup + (R & (kGroup - 1))) * (1 << (sy + sx)) +
+                               ((r & ((1 << sy) - 1)) << sx)) * 4);
+        if constexpr (N == 4)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, val), rs, in ? off : SOOB, 0, 0);
     };
     // Scaling: x = acc 2^(nqe + ext) (/ sqrt(D) when that is no power of two).  Where every
     // exponent of the wave's queries and of the panel's targets lies in [-63, 63], the 2^nqe 2^ext
@@ -1076,7 +1139,7 @@ __global__ __launch_bounds__(NT, 3) void build_kernel(BuildParams P) {
 // Levels beyond the 4 fused ones (num_levels > 4): plain 2x2 floor-mode pooling, tiled in and
 // out, one thread per output pixel.  Not on the E-RAFT path (num_levels = 4, eraft.py:50).
 __global__ __launch_bounds__(256) void pool2_kernel(const float* __restrict__ in, float* __restrict__ out,
-                                                    int64_t rows, int h, int w, int ntx_in, int64_t sz_in,
+                                                    int64_t rows, int h, int w, int lv_in, int ntx_in, int64_t sz_in,
                                                     int ntx_out, int64_t sz_out) {
     const int ho = h / 2, wo = w / 2;
     const int64_t n = rows * ho * wo;
@@ -1084,10 +1147,9 @@ __global__ __launch_bounds__(256) void pool2_kernel(const float* __restrict__ in
         const int64_t rw = i / ((int64_t)ho * wo);
         const int yx = (int)(i - rw * ho * wo);
         const int y = yx / wo, x = yx - y * wo;
-        const float* s = in + rw * sz_in;
+        auto at = [&](int yy, int xx) { return in[pix_off(rw, yy, xx, lv_in, ntx_in, w, sz_in)]; };
         out[rw * sz_out + level_off(y, x, ntx_out, wo)] =
-            pool4(s[level_off(2 * y, 2 * x, ntx_in, w)], s[level_off(2 * y, 2 * x + 1, ntx_in, w)],
-                  s[level_off(2 * y + 1, 2 * x, ntx_in, w)], s[level_off(2 * y + 1, 2 * x + 1, ntx_in, w)]);
+            pool4(at(2 * y, 2 * x), at(2 * y, 2 * x + 1), at(2 * y + 1, 2 * x), at(2 * y + 1, 2 * x + 1));
     }
 }
 
@@ -1190,7 +1252,7 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
         const int64_t n = rows * g.h[i] * g.w[i];
         const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
         hipLaunchKernelGGL(pool2_kernel, dim3(grid), dim3(256), 0, stream, pyramid + g.off[i - 1], pyramid + g.off[i],
-                           rows, g.h[i - 1], g.w[i - 1], g.ntx[i - 1], g.sz[i - 1], g.ntx[i], g.sz[i]);
+                           rows, g.h[i - 1], g.w[i - 1], i - 1, g.ntx[i - 1], g.sz[i - 1], g.ntx[i], g.sz[i]);
         e = hipGetLastError();
         if (e != hipSuccess) return ECORR_EHIP - (int)e;
     }

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/ecorr.h"
+
 namespace ecorr {
 
 constexpr int kWave = 64;
@@ -32,6 +34,26 @@ __host__ __device__ __forceinline__ bool level_compact(int level, int h, int w) 
 // (ntx <= 0, width w).
 __host__ __device__ __forceinline__ int level_off(int y, int x, int ntx, int w) {
     return ntx > 0 ? tiled_off(y, x, ntx) : y * w + x;
+}
+
+// Levels 2 and 3 are stored interleaved (ntx = -nbx < 0): query rows in groups of kGroup = 64, and a
+// group holds, for each (8 >> lv) x (16 >> lv) block of the level image -- what one 8 x 16 target
+// block of level 0 pools to -- that block of its 64 rows back to back: [group][block][row][bh][bw],
+// blocks row-major (nbx per block row).  One build tile then writes each level-2/3 block of its
+// 256 query rows as whole lines (the per-row pieces are 32 / 8 bytes), and the lookup reads a
+// window's blocks with lines shared by adjacent queries.
+constexpr int kGroup = ECORR_ROW_GROUP;
+__host__ __device__ __forceinline__ int ilv_sy(int lv) { return 3 - lv; }   // log2 block height
+__host__ __device__ __forceinline__ int ilv_sx(int lv) { return 4 - lv; }   // log2 block width
+
+// Float offset of pixel (y, x) of query row R (0 .. B*q_count - 1) from the level's base, any
+// format; sz = floats per query image (an interleaved group spans kGroup * sz floats).
+__host__ __device__ __forceinline__ int64_t pix_off(int64_t R, int y, int x, int lv, int ntx, int w, int64_t sz) {
+    if (ntx >= 0) return R * sz + level_off(y, x, ntx, w);
+    const int sy = ilv_sy(lv), sx = ilv_sx(lv);
+    return (R >> 6) * (kGroup * sz) +
+           ((int64_t)((y >> sy) * -ntx + (x >> sx)) * kGroup + (R & (kGroup - 1))) * (1 << (sy + sx)) +
+           ((y & ((1 << sy) - 1)) << sx) + (x & ((1 << sx) - 1));
 }
 
 // model/utils.py:11-12 then ATen grid_sampler unnormalize (align_corners=True):
@@ -66,6 +88,14 @@ __device__ __forceinline__ float corner(const float* __restrict__ img, int h, in
     return img[ntx <= 0 ? (int64_t)y * w + x : (int64_t)tiled_off(y, x, ntx)];
 }
 
+// The same corner fetch from pyramid level lv (base lvbase, any format) for query row R.
+__device__ __forceinline__ float level_corner(const float* __restrict__ lvbase, int64_t R, int lv, int ntx, int h,
+                                              int w, int64_t sz, float fx, float fy) {
+    const bool in = (fx >= 0.0f) & (fx < (float)w) & (fy >= 0.0f) & (fy < (float)h);
+    if (!in) return 0.0f;
+    return lvbase[pix_off(R, (int)fy, (int)fx, lv, ntx, w, sz)];
+}
+
 // One bilinear sample of img[h][w] at pixel coordinates (x, y) (model/utils.py:7-21).
 __device__ __forceinline__ float sample_px(const float* __restrict__ img, int h, int w, float x, float y,
                                            int ntx = 0) {
@@ -76,6 +106,19 @@ __device__ __forceinline__ float sample_px(const float* __restrict__ img, int h,
     const float x1 = __fadd_rn(x0, 1.0f), y1 = __fadd_rn(y0, 1.0f);
     return blend(corner(img, h, w, x0, y0, ntx), corner(img, h, w, x1, y0, ntx),
                  corner(img, h, w, x0, y1, ntx), corner(img, h, w, x1, y1, ntx), wx, wy);
+}
+
+// sample_px on query row R of pyramid level lv (any format).
+__device__ __forceinline__ float sample_level_px(const float* __restrict__ lvbase, int64_t R, int lv, int ntx, int h,
+                                                 int w, int64_t sz, float x, float y) {
+    const float ix = unnormalize(x, (float)(w - 1), (float)(w - 1) * 0.5f);
+    const float iy = unnormalize(y, (float)(h - 1), (float)(h - 1) * 0.5f);
+    const float x0 = floorf(ix), y0 = floorf(iy);
+    const float wx = __fsub_rn(ix, x0), wy = __fsub_rn(iy, y0);
+    const float x1 = __fadd_rn(x0, 1.0f), y1 = __fadd_rn(y0, 1.0f);
+    return blend(level_corner(lvbase, R, lv, ntx, h, w, sz, x0, y0), level_corner(lvbase, R, lv, ntx, h, w, sz, x1, y0),
+                 level_corner(lvbase, R, lv, ntx, h, w, sz, x0, y1), level_corner(lvbase, R, lv, ntx, h, w, sz, x1, y1),
+                 wx, wy);
 }
 
 }  // namespace ecorr

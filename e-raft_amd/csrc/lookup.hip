@@ -145,9 +145,8 @@ __global__ __launch_bounds__(NT) void lookup_direct(LookupParams P, int B) {
         const float inv = 1.0f / (float)(1 << lv);
         const float cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
         const float cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);
-        const float* img = P.lvl[lv] + ((int64_t)b * P.q_count + qq) * (int64_t)P.lsz[lv];
-        P.out[i] = sample_px(img, h, w, __fadd_rn(cx, (float)(a - P.radius)),
-                             __fadd_rn(cy, (float)(bb - P.radius)), P.lntx[lv]);
+        P.out[i] = sample_level_px(P.lvl[lv], (int64_t)b * P.q_count + qq, lv, P.lntx[lv], h, w, P.lsz[lv],
+                                   __fadd_rn(cx, (float)(a - P.radius)), __fadd_rn(cy, (float)(bb - P.radius)));
     }
 }
 

@@ -122,7 +122,10 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const Lookup
     constexpr int S = WS::S, SP = WS::SP;
     const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
     const int64_t hw = P.lsz[lv];  // floats per query image
-    const float* __restrict__ lvbase = P.lvl[lv] + ((int64_t)b * P.q_count + q0) * hw;
+    const int64_t R0 = (int64_t)b * P.q_count + q0;   // first query row of the group
+    // interleaved levels (ntx < 0, ecorr_device.h): the slab starts at the 64-row group of R0
+    const int64_t g0 = R0 >> 6;
+    const float* __restrict__ lvbase = P.lvl[lv] + (ntx < 0 ? g0 * kGroup * hw : R0 * hw);
 
     // ---- phase 1: stage windows, zeros outside the image (grid_sample padding_mode='zeros').
     // Work item = (query, window column); each item walks the S rows.  Loads are raw buffer loads
@@ -132,8 +135,16 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const Lookup
     constexpr int ITEMS = QB * S;
     constexpr int NCOL = (ITEMS + NTQ - 1) / NTQ;
     const int nq = min(QB, P.q_count - q0);
+    const int64_t span = ntx < 0 ? (((R0 + nq - 1) >> 6) - g0 + 1) * kGroup * hw : nq * hw;
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lvbase), 0, (int)(nq * hw * 4), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lvbase), 0, (int)(span * 4), 0x00020000);
+    // row walk down a window column: in-block steps and block-row wraps (tiled: 4 x 8 tiles;
+    // interleaved: bh x bw blocks; compact: every step is a wrap of one image row)
+    const bool tiled = ntx > 0, ilv = ntx < 0;
+    const int sy = ilv ? ilv_sy(lv) : 2, sx = ilv ? ilv_sx(lv) : 3;
+    const int ymask = tiled || ilv ? (1 << sy) - 1 : 0;
+    const int step_in = 4 << sx;
+    const int step_wrap = tiled ? 128 * ntx - 96 : ilv ? 4 * (-ntx * kGroup * (1 << (sy + sx)) - ymask * (1 << sx)) : 4 * w;
     constexpr int OOB = 0x7ffffff0;   // beyond any slab: reads as 0
     float vals[NCOL][S];
     int dst[NCOL];
@@ -150,19 +161,27 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const Lookup
         dst[c] = live ? gq * SP + rx : -1;
         // rows ry in [rlo, rhi) are needed and inside the image; the column's byte offset walks
         // down the rows incrementally (tiled: +8 floats inside a tile, + one tile row minus 24 from
-        // in-tile row 3; compact: +w) instead of re-deriving level_off per row
+        // in-tile row 3; interleaved likewise per block; compact: +w) instead of re-deriving the
+        // offset per row (y0 may be negative: the shift / mask decomposition stays consistent)
         const int rlo = max(0, -y0), rhi = colin ? max(rlo, min(ny, h - y0)) : rlo;   // rhi >= rlo
-        const bool tiled = ntx > 0;
-        const int step_in = tiled ? 32 : 4 * w, step_wrap = tiled ? 128 * ntx - 96 : 4 * w;
-        int off = (int)(gq * hw) * 4 + (tiled ? ((((y0 >> 2) * ntx + (x >> 3)) << 5) + ((y0 & 3) << 3) + (x & 7)) * 4
-                                             : (y0 * w + x) * 4);
-        int ym = y0 & 3;
+        int off;
+        if (tiled) {
+            off = (int)(gq * hw) * 4 + ((((y0 >> 2) * ntx + (x >> 3)) << 5) + ((y0 & 3) << 3) + (x & 7)) * 4;
+        } else if (ilv) {
+            const int64_t Rq = R0 + gq;
+            off = (int)((((Rq >> 6) - g0) * kGroup * hw +
+                         ((int64_t)((y0 >> sy) * -ntx + (x >> sx)) * kGroup + (Rq & (kGroup - 1))) * (1 << (sy + sx)) +
+                         ((y0 & ymask) << sx) + (x & ((1 << sx) - 1))) * 4);
+        } else {
+            off = (int)(gq * hw) * 4 + (y0 * w + x) * 4;
+        }
+        int ym = y0 & ymask;
 #pragma unroll
         for (int ry = 0; ry < S; ++ry) {
             const bool need = (unsigned)(ry - rlo) < (unsigned)(rhi - rlo);
             vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));
-            off += ym == 3 ? step_wrap : step_in;
-            ym = (ym + 1) & 3;
+            off += ym == ymask ? step_wrap : step_in;
+            ym = (ym + 1) & ymask;
         }
     }
 #pragma unroll
@@ -178,10 +197,12 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const Lookup
 __device__ __forceinline__ float sample_direct(const LookupParams& P, int lv, int b, int p, float xa, float yb,
                                                float wa, float nb) {
     const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
-    const float* img = P.lvl[lv] + ((int64_t)b * P.q_count + p) * (int64_t)P.lsz[lv];
+    const int64_t Rq = (int64_t)b * P.q_count + p, sz = P.lsz[lv];
+    const float* base = P.lvl[lv];
     const float xa1 = __fadd_rn(xa, 1.0f), yb1 = __fadd_rn(yb, 1.0f);
-    return blend(corner(img, h, w, xa, yb, ntx), corner(img, h, w, xa1, yb, ntx),
-                 corner(img, h, w, xa, yb1, ntx), corner(img, h, w, xa1, yb1, ntx), wa, nb);
+    return blend(level_corner(base, Rq, lv, ntx, h, w, sz, xa, yb), level_corner(base, Rq, lv, ntx, h, w, sz, xa1, yb),
+                 level_corner(base, Rq, lv, ntx, h, w, sz, xa, yb1), level_corner(base, Rq, lv, ntx, h, w, sz, xa1, yb1),
+                 wa, nb);
 }
 
 // Phase 2: sample k = a(2r+1) + b of query g (staged mode md = 0 or direct mode md = 1).

@@ -1,9 +1,12 @@
-"""Pyramid storage (include/ecorr.h).  Each query image of level i is stored either as row-major
-4 x 8-float tiles (128 bytes, one L2 line) or, for small levels >= 2 where tile padding would
-exceed half the image, compact row-major; `formats` asks libecorr which (ntx = tiles per tile row,
-0 = compact).  `untile` turns a level back into the reference's corr_pyramid shape
-[rows, 1, h, w] (nothing on the E-RAFT path reads corr_pyramid, corr.py:16-27); `tile` and `pack`
-are the inverse, used to feed externally produced pyramids (tests) to ecorr_lookup."""
+"""Pyramid storage (include/ecorr.h).  Each query image of levels 0-1 (and >= 4) is stored as
+row-major 4 x 8-float tiles (128 bytes, one L2 line) or, for small levels >= 4 where tile padding
+would exceed half the image, compact row-major; levels 2 and 3 are interleaved: query rows in
+groups of 64, each group storing every (8 >> i) x (16 >> i) block of the level for its 64 rows back
+to back.  `formats` asks libecorr which (ntx = tiles per tile row, 0 = compact, -nbx =
+interleaved with nbx blocks per block row).  `untile` turns a level back into the reference's
+corr_pyramid shape [rows, 1, h, w] (nothing on the E-RAFT path reads corr_pyramid,
+corr.py:16-27); `tile` and `pack` are the inverse, used to feed externally produced pyramids
+(tests) to ecorr_lookup."""
 import ctypes
 
 import torch
@@ -17,29 +20,53 @@ def padded(h, w):
     return -(-h // TILE_H) * TILE_H, -(-w // TILE_W) * TILE_W
 
 
+GROUP = 64   # query rows per interleave group (ecorr_device.h kGroup)
+
+
+def block_shape(level):
+    """(bh, bw) of an interleaved level's blocks: what one 8 x 16 level-0 target block pools to."""
+    assert level in (2, 3), level
+    return 8 >> level, 16 >> level
+
+
 def formats(H, W, levels):
-    """ntx per level: tiles per tile row, or 0 for a compact row-major level."""
+    """ntx per level: tiles per tile row, 0 for a compact row-major level, -nbx for an
+    interleaved level (nbx blocks per block row)."""
     ntx = (ctypes.c_int * levels)()
     _lib.check(_lib.lib().ecorr_pyramid_formats(H, W, levels, ntx), "CorrBlock pyramid")
     return list(ntx)
 
 
-def untile(flat, rows, h, w, ntx):
+def untile(flat, rows, h, w, ntx, level=None):
     """flat level storage -> [rows, 1, h, w] tensor in the reference layout (a view when the
-    level is compact, a copy when tiled)."""
+    level is compact, a copy when tiled or interleaved; interleaved levels need `level`)."""
     if ntx == 0:
         return flat[:rows * h * w].view(rows, 1, h, w)
+    if ntx < 0:
+        bh, bw = block_shape(level)
+        nbx, nby = -ntx, -(-h // bh)
+        ng = -(-rows // GROUP)
+        t = flat[:ng * nby * nbx * GROUP * bh * bw].view(ng, nby, nbx, GROUP, bh, bw).permute(0, 3, 1, 4, 2, 5)
+        return t.reshape(ng * GROUP, nby * bh, nbx * bw)[:rows, :h, :w].contiguous().view(rows, 1, h, w)
     hp, wp = padded(h, w)
     t = flat[:rows * hp * wp].view(rows, hp // TILE_H, wp // TILE_W, TILE_H, TILE_W).permute(0, 1, 3, 2, 4)
     return t.reshape(rows, hp, wp)[:, :h, :w].contiguous().view(rows, 1, h, w)
 
 
-def tile(level, ntx=1):
-    """[rows, h, w] (or [rows, 1, h, w]) reference-layout level -> flat storage (zero pad)."""
+def tile(level, ntx=1, index=None):
+    """[rows, h, w] (or [rows, 1, h, w]) reference-layout level -> flat storage (zero pad);
+    interleaved formats (ntx < 0) need the level's `index`."""
     level = torch.as_tensor(level)
     rows, h, w = level.shape[0], level.shape[-2], level.shape[-1]
     if ntx == 0:
         return level.reshape(-1).contiguous()
+    if ntx < 0:
+        bh, bw = block_shape(index)
+        nbx, nby = -ntx, -(-h // bh)
+        ng = -(-rows // GROUP)
+        buf = level.new_zeros((ng * GROUP, nby * bh, nbx * bw))
+        buf[:rows, :h, :w] = level.reshape(rows, h, w)
+        return buf.view(ng, GROUP, nby, bh, nbx, bw).permute(0, 2, 4, 1, 3, 5).reshape(-1)
     hp, wp = padded(h, w)
     buf = level.new_zeros((rows, hp, wp))
     buf[:, :h, :w] = level.reshape(rows, h, w)
@@ -55,6 +82,13 @@ def pack(levels, H, W):
     ntx = formats(H, W, n)
     buf = torch.zeros(off[-1], dtype=torch.float32)
     for i, lv in enumerate(levels):
-        t = tile(torch.as_tensor(lv), ntx[i])
+        t = tile(torch.as_tensor(lv), ntx[i], i)
         buf[off[i]:off[i] + t.numel()] = t
     return buf
+
+
+def levels_of(pyramid, rows, H, W, levels):
+    """The flat pyramid of `rows` query rows -> reference-layout levels [rows, 1, h_i, w_i]."""
+    h, w, off = _lib.layout(rows, H, W, levels)
+    ntx = formats(H, W, levels)
+    return [untile(pyramid[off[i]:off[i + 1]], rows, h[i], w[i], ntx[i], i) for i in range(levels)]

@@ -182,7 +182,7 @@ class RowShardedCorrBlock:
             rows = self._shape[0] * self.q_count
             ntx = formats(self._shape[2], self._shape[3], self.num_levels)
             self._levels_cache = [
-                untile(self._pyramid[self._off[i]:self._off[i + 1]], rows, self._h[i], self._w[i], ntx[i])
+                untile(self._pyramid[self._off[i]:self._off[i + 1]], rows, self._h[i], self._w[i], ntx[i], i)
                 for i in range(self.num_levels)]
         return self._levels_cache
 

@@ -12,15 +12,21 @@
  * `levels` blocks concatenated at float offsets off_i (each a multiple of 32 floats, i.e. 128-byte
  * aligned); level i holds rows = B * q_count query images of h_i x w_i (h_0 = H, w_0 = W,
  * h_{i+1} = h_i / 2, w_{i+1} = w_i / 2, floor -- the shapes of the reference's corr_pyramid[i],
- * corr.py:16-27).  Each image is stored in one of two formats (ecorr_pyramid_formats):
- *   tiled (ntx_i > 0): row-major ECORR_TILE_H x ECORR_TILE_W tiles of 32 floats (128 bytes, one
- *     L2 line); image r starts at off_i + r * hp_i * wp_i, hp_i = roundup(h_i, 4),
- *     wp_i = roundup(w_i, 8) = 8 * ntx_i, and pixel (y, x) sits at
+ * corr.py:16-27).  Each level is stored in one of three formats (ecorr_pyramid_formats):
+ *   tiled (ntx_i > 0; levels 0, 1 and >= 4): row-major ECORR_TILE_H x ECORR_TILE_W tiles of 32
+ *     floats (128 bytes, one L2 line); image r starts at off_i + r * hp_i * wp_i,
+ *     hp_i = roundup(h_i, 4), wp_i = roundup(w_i, 8) = 8 * ntx_i, and pixel (y, x) sits at
  *     ((y / 4) * ntx_i + x / 8) * 32 + (y % 4) * 8 + x % 8.  A radius-4 window then touches ~7
  *     lines per level instead of ~13 with row-major images; padding cells are never read.
+ *   interleaved (ntx_i = -nbx < 0; levels 2 and 3): blocks of bh x bw = (8 >> i) x (16 >> i)
+ *     pixels (what one 8 x 16 block of level 0 pools to), nby = ceil(h_i / bh) by nbx =
+ *     ceil(w_i / bw) of them per image, sz = nby * nbx * bh * bw floats per image; the rows are
+ *     taken in groups of ECORR_ROW_GROUP = 64 (the level holds roundup(rows, 64) * sz floats) and
+ *     pixel (y, x) of row r sits at (r / 64) * 64 * sz + (((y / bh) * nbx + x / bw) * 64 + r % 64)
+ *     * bh * bw + (y % bh) * bw + x % bw: a block's pixels of 64 consecutive rows are contiguous,
+ *     so the build stores them as whole lines and adjacent queries' window reads share lines.
  *   compact (ntx_i = 0): plain row-major h_i x w_i, image r at off_i + r * h_i * w_i.  Used for
- *     levels i >= 2 whose tile padding would exceed half the image (2 hp wp > 3 h w; DSEC level
- *     3: 7 x 10), where the window covers most of the image anyway.
+ *     levels i >= 4 whose tile padding would exceed half the image (2 hp wp > 3 h w).
  * The Python shim materializes reference-layout corr_pyramid views on demand.
  *
  * Query slabs (multi-GPU query-row sharding): fmap1, coords and the lookup output hold
@@ -36,10 +42,11 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 11
+#define ECORR_ABI_VERSION 12
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
+#define ECORR_ROW_GROUP 64
 
 enum ecorr_status {
     ECORR_OK = 0,
@@ -190,8 +197,9 @@ int ecorr_voxel_grid_mvsec(const double* events, int64_t n, int C, int H, int W,
 /* Tile shape of the pyramid storage (ECORR_TILE_H, ECORR_TILE_W). */
 int ecorr_pyramid_tile(int* tile_h, int* tile_w);
 
-/* Storage format of each level of an H x W pyramid: ntx[i] = tiles per tile row (tiled) or 0
- * (compact row-major).  Same errors as ecorr_pyramid_layout. */
+/* Storage format of each level of an H x W pyramid: ntx[i] = tiles per tile row (tiled), 0
+ * (compact row-major) or -nbx (interleaved, nbx blocks per block row).  Same errors as
+ * ecorr_pyramid_layout. */
 int ecorr_pyramid_formats(int H, int W, int levels, int* ntx);
 
 /* Human-readable name of a status code (static storage). */

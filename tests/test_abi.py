@@ -61,17 +61,22 @@ def test_layout_matches_reference_shapes(ea):
     from eraft_amd import _lib
     h, w, off = _lib.layout(16 * 4800, 60, 80, 4)
     assert (h, w) == ([60, 30, 15, 7], [80, 40, 20, 10])
-    # levels 0-2 tiled (each image padded to 4 x 8 tiles: 60x80, 32x40, 16x24); level 3 (7 x 10,
-    # tiles would pad it to 8 x 16) compact row-major; every level starts on a 128-byte line
-    sizes = [60 * 80, 32 * 40, 16 * 24, 7 * 10]
+    # levels 0-1 tiled (each image padded to 4 x 8 tiles: 60x80, 32x40); levels 2-3 interleaved in
+    # 2 x 4 / 1 x 2 blocks (15 x 20 -> 8 x 5 blocks, 7 x 10 -> 7 x 5); every level starts on a
+    # 128-byte line
+    sizes = [60 * 80, 32 * 40, 8 * 5 * 8, 7 * 5 * 2]
     assert off == [0] + list(np.cumsum([76800 * s for s in sizes]))
     from eraft_amd.layout import formats
-    assert formats(60, 80, 4) == [10, 5, 3, 0]
-    assert formats(32, 32, 4) == [4, 2, 1, 0]        # MVSEC: 4 x 4 level 3 compact
-    assert formats(92, 160, 4) == [20, 10, 5, 3]     # 1280x720: 11 x 20 level 3 stays tiled
-    _, _, off = _lib.layout(3, 20, 20, 4)            # compact 5x5 / 2x2 levels: starts rounded to 32
-    assert formats(20, 20, 4) == [3, 2, 0, 0]
-    assert off == [0, 1440, 2016, 2112, 2144]
+    assert formats(60, 80, 4) == [10, 5, -5, -5]
+    assert formats(32, 32, 4) == [4, 2, -2, -2]       # MVSEC: 8 x 8 and 4 x 4 levels
+    assert formats(92, 160, 4) == [20, 10, -10, -10]  # 1280x720: 23 x 40 and 11 x 20 levels
+    # 3 rows: interleaved levels hold whole 64-row groups (5x5 -> 3 x 2 blocks of 8, 2x2 -> 2 x 1 of 2)
+    _, _, off = _lib.layout(3, 20, 20, 4)
+    assert formats(20, 20, 4) == [3, 2, -2, -1]
+    assert off == [0, 1440, 2016, 2016 + 64 * 48, 2016 + 64 * 48 + 64 * 4]
+    # levels past 3 stay tiled, or compact where tiles would pad them by more than half
+    assert formats(64, 64, 6) == [8, 4, -4, -4, 0, 0]
+    assert formats(128, 256, 6) == [32, 16, -16, -16, 2, 1]
     th, tw = ctypes.c_int(), ctypes.c_int()
     assert ea.lib().ecorr_pyramid_tile(ctypes.byref(th), ctypes.byref(tw)) == 0
     assert (th.value, tw.value) == (4, 8)
@@ -132,6 +137,25 @@ def test_tile_untile_roundtrip():
         # element (y, x) of image r lives at r*hp*wp + ((y//4)*(wp//8) + x//8)*32 + (y%4)*8 + x%8
         r, y, x = 2, h - 1, w - 1
         assert flat[r * hp * wp + ((y // 4) * (wp // 8) + x // 8) * 32 + (y % 4) * 8 + x % 8] == lv[r, y, x]
+
+
+def test_interleaved_roundtrip():
+    """Levels 2-3: [64-row group][block][row][bh][bw] (include/ecorr.h), ragged rows and sides."""
+    import torch
+    from eraft_amd.layout import GROUP, tile, untile
+    for level, (bh, bw) in ((2, (2, 4)), (3, (1, 2))):
+        for rows, h, w in [(3, 15, 20), (130, 7, 10), (64, 1, 1), (65, 5, 9)]:
+            lv = torch.arange(rows * h * w, dtype=torch.float32).reshape(rows, h, w)
+            nbx, nby = -(-w // bw), -(-h // bh)
+            flat = tile(lv, ntx=-nbx, index=level)
+            ng = -(-rows // GROUP)
+            assert flat.numel() == ng * GROUP * nby * nbx * bh * bw
+            assert torch.equal(untile(flat, rows, h, w, -nbx, level)[:, 0], lv)
+            sz = nby * nbx * bh * bw
+            for r, y, x in [(rows - 1, h - 1, w - 1), (0, 0, 0), (rows // 2, h // 2, w - 1)]:
+                off = ((r // GROUP) * GROUP * sz + (((y // bh) * nbx + x // bw) * GROUP + r % GROUP) * bh * bw
+                       + (y % bh) * bw + x % bw)
+                assert flat[off] == lv[r, y, x]
 
 
 def test_split_build_arguments(ea):

@@ -49,7 +49,7 @@ def _build(ea, f1, f2, mode, levels=4):
     from eraft_amd.layout import formats, untile
     h, w, _ = _lib.layout(B * H * W, H, W, levels)
     ntx = formats(H, W, levels)
-    return [untile(pyr[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i])[:, 0].cpu().numpy()
+    return [untile(pyr[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i], i)[:, 0].cpu().numpy()
             for i in range(levels)]
 
 
@@ -93,7 +93,7 @@ def test_split_query_slab_matches_whole(ea):
     h, w, _ = _lib.layout(B * q, H, W, 4)
     ntx = formats(H, W, 4)
     for i in range(4):
-        got = untile(pyr[off[i]:off[i + 1]], B * q, h[i], w[i], ntx[i])[:, 0].cpu().numpy()
+        got = untile(pyr[off[i]:off[i + 1]], B * q, h[i], w[i], ntx[i], i)[:, 0].cpu().numpy()
         want = whole[i].reshape(B, H * W, h[i], w[i])[:, r0 * W:(r0 + rr) * W].reshape(B * q, h[i], w[i])
         assert oracle.same_bits(got, want), f"level {i}"
 
@@ -216,6 +216,6 @@ def test_split_two_stage_calls_match_one(ea):
     h, w, _ = _lib.layout(B * H * W, H, W, 4)
     ntx = formats(H, W, 4)
     for i in range(4):
-        a = untile(one[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i])
-        b = untile(two[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i])
+        a = untile(one[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i], i)
+        b = untile(two[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i], i)
         assert torch.equal(a, b), f"level {i}"

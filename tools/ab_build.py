@@ -49,7 +49,7 @@ def levels_of(lib, f1, f2, levels=4):
     h, w, off = _lib.layout(B * H * W, H, W, levels)
     pyr = _lib.build_pyramid(f1, f2, B, D, H, W, H * W, levels, off, "ab build", mode=MODE)
     ntx = formats(H, W, levels)
-    return [untile(pyr[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i]) for i in range(levels)]
+    return [untile(pyr[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i], i) for i in range(levels)]
 
 
 def main():

@@ -247,6 +247,15 @@ PATCHES["loopstamps16"] = [
     __builtin_amdgcn_s_barrier();   // every wave is done with the ring"""),
     ("build.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + STAMP_EXPORT),
 ]
+# the tree as it is (the baseline of an A/B against an edited tree)
+PATCHES["base"] = []
+# round-2 store ablations on the current epilogue (timing only): level-2/3 pixel stores issued out
+# of range / as non-temporal stores; level-0/1 line stores out of range
+_L23 = ["__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, 0);",
+        "__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, val), rs, in ? off : SOOB, 0, 0);"]
+PATCHES["l23oob"] = [("build.hip", s, s.replace("in ? off : SOOB", "in ? SOOB : SOOB")) for s in _L23]
+PATCHES["l23nt"] = [("build.hip", s, s.replace(", 0, 0);", ", 0, 2);")) for s in _L23]
+PATCHES["l01oob"] = [("build.hip", "ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_L01);", "ok ? SOOB : SOOB, 0, ST_L01);")]
 COMBOS = {"loopstamps_epioob": ["loopstamps", "epioob"], "stamps_loopprio": ["stamps", "loopprio"], "stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
 COMBOS.update({"loopstamps_qwait": ["loopstamps", "qwait"]})
 COMBOS.update({"stamps_epi_noscale": ["stamps", "epi_noscale"], "stamps_epi_nolds": ["stamps", "epi_nolds"]})
