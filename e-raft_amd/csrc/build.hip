@@ -148,7 +148,9 @@ __device__ __forceinline__ float* level_px(const BuildParams& P, int L, int64_t 
 // ============================================================================================
 constexpr int SQ = 256;                     // queries per split tile
 constexpr int SCHUNK = PANEL;               // LDS bytes per K chunk (the target panel)
-constexpr int SNBUF = 3;
+constexpr int SDT = 4;                      // target panel: chunks ahead = LDS buffers (NK > 0 loop)
+constexpr int SDQ = 3;                      // query fragments: chunks ahead = register sets (NK > 0 loop)
+constexpr int SNBUF = SDT;
 constexpr int SCOPIES = SCHUNK / 1024 / 4;  // LDS-DMA copies per wave per chunk (2)
 constexpr int QLOADS = 4;                   // query fragment loads per wave per chunk (hi, lo x 2 rows)
 constexpr int SLDS = 4 * 4 * 32 * 144;      // LDS bytes: the epilogue's transpose regions (> the K loop's)
@@ -166,6 +168,38 @@ __host__ __device__ __forceinline__ void split_target(int p, bool band, int& y, 
     } else {
         y = (p >> 3) & 3;
         x = 8 * (p >> 5) + (p & 7);
+    }
+}
+
+// VMEM instructions a wave has issued after t(j) when the NK > 0 loop's advance(j) waits for it
+// (chunk j - 1, before its own t issue): the issue order of build_split_kernel replayed at compile
+// time (t = SCOPIES LDS-DMA pieces, q = QLOADS fragment loads; q(k) exists for k < nk).
+constexpr int split_vm_after(int j, int nk) {
+    int n = 0;
+    bool seen = false;
+    for (int k = 0; k < SDT; ++k) {   // prologue: t(k) q(k)
+        if (seen) n += SCOPIES;
+        if (k == j) seen = true;
+        if (k < SDQ && k < nk && seen) n += QLOADS;
+    }
+    for (int c = 0; c <= j - 2; ++c) {   // chunk c: t(c + SDT), q(c + SDQ)
+        if (seen) n += SCOPIES;
+        if (c + SDT == j) seen = true;
+        if (c + SDQ < nk && seen) n += QLOADS;
+    }
+    return n;
+}
+static_assert(SDT != 4 || SDQ != 3 ||
+                  (split_vm_after(0, 16) == 18 && split_vm_after(5, 16) == 16 && split_vm_after(16, 16) == 8),
+              "split loop wait counts (hand-checked for SDT 4, SDQ 3)");
+static_assert(split_vm_after(0, 16) < 41, "wait_vm_n range");
+
+// wait_vm<n> for an n that is a constant once the loop around the call is unrolled
+template <bool LGKM0, int N = 40>
+__device__ __forceinline__ void wait_vm_n(int n) {
+    if constexpr (N >= 0) {
+        if (n == N) wait_vm<N, LGKM0>();
+        else wait_vm_n<LGKM0, N - 1>(n);
     }
 }
 
@@ -315,53 +349,45 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
     };
 
     if constexpr (NK > 0) {
-        // D known at compile time: query fragments two chunks ahead in three register sets.  VMEM
-        // issue order per wave t(0) q(0) t(1) q(1) | t(2) q(2) | t(3) q(3) ...: chunk c issues
-        // t(c + 3) in advance(c + 1) and q(c + 3) at its end, so at advance(j)'s wait the 10 younger
-        // q(j), t(j + 1), q(j + 1) may fly.
+        // D known at compile time: the target panel SDT chunks ahead (SDT LDS buffers), the query
+        // fragments SDQ chunks ahead in SDQ register sets.  VMEM issue order per wave: prologue
+        // t(0) q(0) t(1) q(1) ... t(SDT - 1), then chunk c issues t(c + SDT) in advance(c + 1) and
+        // q(c + SDQ) at its end; advance(j)'s wait count is split_vm_after(j) (loads past the last
+        // chunk are not issued: hipcc deletes loads whose registers are never read).
         TFrags f[2];
-        QFrags qs[3];
-        // (no query loads past the last chunk: hipcc deletes loads whose registers are never read,
-        // so the waits count only the loads that exist)
-        auto advance3 = [&](int j) {
+        QFrags qs[SDQ];
+        auto advance_n = [&](int j) {
             PHASE;
-            if (j + 1 < NK) wait_vm<QLOADS + SCOPIES + QLOADS, true>();
-            else if (j < NK) wait_vm<QLOADS + SCOPIES, true>();
-            else wait_vm<SCOPIES, true>();
+            wait_vm_n<true>(split_vm_after(j, NK));
             __builtin_amdgcn_s_barrier();
             PHASE;
-            issue(j + 2);
+            issue(j + SDT - 1);
             PHASE;
         };
-        issue(0);
-        PHASE;
-        load_q(0, qs[0]);
-        PHASE;
-        issue(1);
-        PHASE;
-        load_q(1, qs[1]);
-        PHASE;
-        wait_vm<QLOADS + SCOPIES + QLOADS, true>();   // t(0) landed
+#pragma unroll
+        for (int k = 0; k < SDT; ++k) {
+            issue(k);
+            PHASE;
+            if (k < SDQ) load_q(k, qs[k]);
+            PHASE;
+        }
+        wait_vm_n<true>(split_vm_after(0, NK));   // t(0) landed
         __builtin_amdgcn_s_barrier();
-        PHASE;
-        issue(2);
         PHASE;
         read_lo(0, f[0]);
         read_hi(0, f[0]);
         PHASE;
-        load_q(2, qs[2]);
-        PHASE;
 #pragma unroll
         for (int kc = 0; kc < NK; ++kc) {
-            mfma_lohi(f[kc & 1], qs[kc % 3]);
+            mfma_lohi(f[kc & 1], qs[kc % SDQ]);
             PHASE;
-            advance3(kc + 1);
+            advance_n(kc + 1);
             read_lo(kc + 1, f[(kc + 1) & 1]);
             PHASE;
-            mfma_rest(f[kc & 1], qs[kc % 3]);
+            mfma_rest(f[kc & 1], qs[kc % SDQ]);
             PHASE;
             read_hi(kc + 1, f[(kc + 1) & 1]);
-            if (kc + 3 < NK) load_q(kc + 3, qs[kc % 3]);
+            if (kc + SDQ < NK) load_q(kc + SDQ, qs[kc % SDQ]);
             PHASE;
         }
     } else {
@@ -453,8 +479,9 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
     };
     // One block row (r, c .. c + N - 1), N = the block width, of level 2 or 3 (interleaved) for
     // block-local query qloc: lanes on consecutive queries write consecutive 4N-byte pieces, so a
-    // store instruction covers whole lines.  Queries past the block and blocks outside the level
-    // are dropped (padding cells of a block are written and never read).
+    // store instruction covers whole lines, which leave non-temporally like levels 0-1 (A/B: 656
+    // vs 685 us with plain stores, which park the lines in L2).  Queries past the block and
+    // blocks outside the level are dropped (padding cells of a block are written, never read).
     auto store_px = [&](__amdgpu_buffer_rsrc_t rs, int lv, int qloc, int r, int c, auto val) {
         constexpr int N = sizeof(val) / 4;
         const int sy = ilv_sy(lv), sx = ilv_sx(lv);
@@ -465,9 +492,9 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
                                ((int64_t)(by * -P.lntx[lv] + bx) * kGroup + (R & (kGroup - 1))) * (1 << (sy + sx)) +
                                ((r & ((1 << sy) - 1)) << sx)) * 4);
         if constexpr (N == 4)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, ST_L01);
         else
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, val), rs, in ? off : SOOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, val), rs, in ? off : SOOB, 0, ST_L01);
     };
     // Scaling: x = acc 2^(nqe + ext) (/ sqrt(D) when that is no power of two).  Where every
     // exponent of the wave's queries and of the panel's targets lies in [-63, 63], the 2^nqe 2^ext

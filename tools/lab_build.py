@@ -256,9 +256,24 @@ _L23 = ["__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val),
 PATCHES["l23oob"] = [("build.hip", s, s.replace("in ? off : SOOB", "in ? SOOB : SOOB")) for s in _L23]
 PATCHES["l23nt"] = [("build.hip", s, s.replace(", 0, 0);", ", 0, 2);")) for s in _L23]
 PATCHES["l01oob"] = [("build.hip", "ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_L01);", "ok ? SOOB : SOOB, 0, ST_L01);")]
+# round-2 K-loop ablations (timing only): no per-chunk barrier; the target-panel DMA / the query
+# fragment loads issued out of range (same instructions and wait counts, no memory traffic)
+PATCHES["nobar"] = [("build.hip", "            else wait_vm<SCOPIES, true>();\n            __builtin_amdgcn_s_barrier();",
+                     "            else wait_vm<SCOPIES, true>();")]
+PATCHES["dmaoob"] = [("build.hip", "in ? kc * PANEL + c * 1024 + lane * 16 : SOOB, 0, 0, 0);", "in ? SOOB : SOOB, 0, 0, 0);")]
+PATCHES["qoob"] = [("build.hip", "rq, in ? qgo + kc * PANEL + i * 2048 : SOOB, 0, 0));", "rq, in ? SOOB : SOOB, 0, 0));"),
+                   ("build.hip", "rq, in ? qgo + kc * PANEL + i * 2048 + 1024 : SOOB, 0, 0));", "rq, in ? SOOB : SOOB, 0, 0));")]
+# split-loop prefetch depth of the target panel (tree: 4 chunks / buffers)
+for _dt in (3, 5, 6):
+    PATCHES[f"dt{_dt}"] = [("build.hip", "constexpr int SDT = 4; ", f"constexpr int SDT = {_dt}; ")]
+# timing only: every block reads the same query / target panels (all L2 hits, same traffic to the CUs)
+PATCHES["sameq"] = [("build.hip", "P.pk1 + ((int64_t)b * P.n_mt + qp) * pstride", "P.pk1")]
+PATCHES["samet"] = [("build.hip", "P.pk2 + ((int64_t)b * P.n_nt + nt) * pstride", "P.pk2")]
 COMBOS = {"loopstamps_epioob": ["loopstamps", "epioob"], "stamps_loopprio": ["stamps", "loopprio"], "stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
 COMBOS.update({"loopstamps_qwait": ["loopstamps", "qwait"]})
 COMBOS.update({"stamps_epi_noscale": ["stamps", "epi_noscale"], "stamps_epi_nolds": ["stamps", "epi_nolds"]})
+COMBOS.update({"sameqt": ["sameq", "samet"]})
+COMBOS.update({"dmaqoob": ["dmaoob", "qoob"], "noepi_r2": ["noepi"]})
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"], "loopstamps_noepi_mfma16": ["loopstamps", "noepi", "mfma16"]})
 
 
