@@ -210,6 +210,224 @@ __device__ __forceinline__ void swap32(float& a, float& b) {
     b = __uint_as_float(r[1]);
 }
 
+// Epilogue of the split build for one wave: its 64 queries (block-local qw .. qw + 63) x the
+// n-tile tc, from its accumulators (C^T fragments, build_split_kernel); xw = the wave's four
+// LDS transpose regions (4 x 32 x XS bytes); exq = the block's query exponents, ext / fst = the
+// n-tile's negated target exponents and their powers of two.
+template <bool MUL>
+__device__ __forceinline__ void split_epilogue(const BuildParams& P, floatx16 (&acc)[2][4], char* const xw, int qw,
+                                               const int* exq, const int* ext, const float* fst, const NTile& tc,
+                                               int b, int q0, int lane) {
+    const int acol = lane & 31, arow = lane >> 5;
+    // Line segments through a wave-private LDS transpose (no barrier: a wave's LDS accesses are
+    // processed in order): the lane writes its 16-byte pieces into the line image of its query
+    // (32 queries x 144 B: conflict-free ds_write_b128 and ds_read_b128), then reads back piece m
+    // of segment arow of query 4k + s, so the 4 lanes of a quad store 64 contiguous bytes and
+    // lanes acol, acol + 32 the two halves of one line.
+    // four regions per wave (one per level-0 line of a tile row; the level-1 line reuses region
+    // 0): no line waits for the previous line's read-back before writing
+    const int m4 = lane & 3, k4 = acol >> 2;
+    const int wo = acol * XS, ro = (4 * k4) * XS + 64 * arow + 16 * m4;
+    const int L = P.fused_levels;
+    const int64_t rows0 = (int64_t)b * P.q_count + q0;   // the block's first query image
+    const int nq = min(SQ, P.q_count - q0);
+    // per-level descriptors over the block's query images (range check = query bound); levels 2-3
+    // (interleaved): over the 64-row groups the block's rows touch, from group g0 = rows0 / 64
+    const int64_t g0 = rows0 >> 6;
+    auto rsrc_of = [&](int lv) {
+        if (lv >= 2)
+            return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + g0 * kGroup * P.lsz[lv], 0,
+                                                     (int)((((rows0 + nq - 1) >> 6) - g0 + 1) * kGroup * P.lsz[lv] * 4),
+                                                     0x00020000);
+        return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + rows0 * P.lsz[lv], 0, (int)(nq * P.lsz[lv] * 4), 0x00020000);
+    };
+    // read the transposed segments back and store them: line byte offset lo (+ the query image)
+    auto store_lines = [&](const char* xp, __amdgpu_buffer_rsrc_t rs, int64_t lsz, int ql, int lo, bool ok) {
+        floatx4 pc[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) pc[s] = *reinterpret_cast<const floatx4*>(xp + ro + s * XS);
+        const int base = (int)((ql + 4 * k4) * lsz * 4) + lo + 16 * m4;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, pc[s]), rs,
+                                                   ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_L01);
+    };
+    // One block row (r, c .. c + N - 1), N = the block width, of level 2 or 3 (interleaved) for
+    // block-local query qloc: lanes on consecutive queries write consecutive 4N-byte pieces, so a
+    // store instruction covers whole lines, which leave non-temporally like levels 0-1 (A/B: 656
+    // vs 685 us with plain stores, which park the lines in L2).  Queries past the block and
+    // blocks outside the level are dropped (padding cells of a block are written, never read).
+    auto store_px = [&](__amdgpu_buffer_rsrc_t rs, int lv, int qloc, int r, int c, auto val) {
+        constexpr int N = sizeof(val) / 4;
+        const int sy = ilv_sy(lv), sx = ilv_sx(lv);
+        const int by = r >> sy, bx = c >> sx;
+        const bool in = qloc < nq && by < P.lnty[lv] && bx < -P.lntx[lv];
+        const int64_t R = rows0 + qloc;
+        const int off = (int)((((R >> 6) - g0) * kGroup * P.lsz[lv] +
+                               ((int64_t)(by * -P.lntx[lv] + bx) * kGroup + (R & (kGroup - 1))) * (1 << (sy + sx)) +
+                               ((r & ((1 << sy) - 1)) << sx)) * 4);
+        if constexpr (N == 4)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, ST_L01);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, val), rs, in ? off : SOOB, 0, ST_L01);
+    };
+    // Scaling: x = acc 2^(nqe + ext) (/ sqrt(D) when that is no power of two).  Where every
+    // exponent of the wave's queries and of the panel's targets lies in [-63, 63], the 2^nqe 2^ext
+    // product is a normal power of two and one multiply by it rounds exactly as ldexpf does: two
+    // packed multiplies per element pair instead of an add, a negate and an ldexp per element.
+    bool fast_scale;
+    {
+        bool ok = ext[lane] >= -63 && ext[lane] <= 63 && ext[lane + 64] >= -63 && ext[lane + 64] <= 63;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int n = -(exq[qw + 32 * i + acol] + (MUL ? P.scale_shift : 0));
+            ok = ok && n >= -63 && n <= 63;
+        }
+        fast_scale = __all(ok);
+    }
+    const __amdgpu_buffer_rsrc_t r0 = rsrc_of(0);
+    const __amdgpu_buffer_rsrc_t r1 = rsrc_of(L > 1 ? 1 : 0);
+    const __amdgpu_buffer_rsrc_t r2 = rsrc_of(L > 2 ? 2 : 0);
+    const __amdgpu_buffer_rsrc_t r3 = rsrc_of(L > 3 ? 3 : 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ql = qw + 32 * i;          // first block-local query of this tile row
+        const int nqe = -(exq[ql + acol] + (MUL ? P.scale_shift : 0));
+        // level-1 values of the lane's query: [block bb][row][col pair] (band: [half][2 y1 + jl]);
+        // level 2: [bb][row r] (band: [bb][jl]); level 3: [bb]
+        float l1[2][4][2], l2[2][2], l3[2];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            // scaled values of lines j = 2 bb + jl, [jl][g4][t]; target exponents
+            // ext[32 j + 8 g4 + 4 arow + t]
+            float v[2][4][4];
+            if (fast_scale) {
+                const float sq = exp2i(nqe);
+#pragma unroll
+                for (int jl = 0; jl < 2; ++jl) {
+                    const int j = 2 * bb + jl;
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        const floatx4 s4 = *reinterpret_cast<const floatx4*>(fst + 32 * j + 8 * g4 + 4 * arow);
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const float x = __fmul_rn(acc[i][j][4 * g4 + t], __fmul_rn(sq, s4[t]));
+                            v[jl][g4][t] = MUL ? x : __fdiv_rn(x, P.scale);
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int jl = 0; jl < 2; ++jl) {
+                    const int j = 2 * bb + jl;
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        const int4 e4 = *reinterpret_cast<const int4*>(ext + 32 * j + 8 * g4 + 4 * arow);
+                        const int e[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const float x = ldexpf(acc[i][j][4 * g4 + t], nqe + e[t]);
+                            v[jl][g4][t] = MUL ? x : __fdiv_rn(x, P.scale);
+                        }
+                    }
+                }
+            }
+            // level 0: line j = rows g4 x this lane's 4 columns
+#pragma unroll
+            for (int jl = 0; jl < 2; ++jl) {
+                const int j = 2 * bb + jl;
+                char* const xp = xw + j * (32 * XS);
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4)
+                    *reinterpret_cast<floatx4*>(xp + wo + 32 * g4 + 16 * arow) =
+                        floatx4{v[jl][g4][0], v[jl][g4][1], v[jl][g4][2], v[jl][g4][3]};
+                const int tr = (tc.ty0 >> 2) + (tc.band ? 0 : (j & 1));
+                const int tcl = (tc.tx0 >> 3) + (tc.band ? j : (j >> 1));
+                store_lines(xp, r0, P.lsz[0], ql, ((tr * P.lntx[0] + tcl) * kTile) * 4 + 64 * arow,
+                            tr < P.lnty[0] && tcl < P.lntx[0]);
+            }
+            if (L < 2) continue;
+            if (!tc.band) {
+                // regular: line j = rows 4 jl + g4 of 8 x 8 block bb; level 1 rows y1 = 0..3, cols
+                // 4 bb + 2 arow + c; level 2 rows r, col 2 bb + arow; level 3 needs lane acol + 32
+#pragma unroll
+                for (int y1 = 0; y1 < 4; ++y1)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int jl = y1 >> 1, g = 2 * (y1 & 1);
+                        l1[bb][y1][c] = pool4_v(v[jl][g][2 * c], v[jl][g][2 * c + 1], v[jl][g + 1][2 * c],
+                                              v[jl][g + 1][2 * c + 1]);
+                    }
+                if (L >= 3) {   // level 2: rows r, col 2 bb + arow (stored per i below)
+#pragma unroll
+                    for (int r = 0; r < 2; ++r)
+                        l2[bb][r] = pool4_v(l1[bb][2 * r][0], l1[bb][2 * r][1], l1[bb][2 * r + 1][0], l1[bb][2 * r + 1][1]);
+                    // level 3, the 8 x 8 pool: lane acol + 32 holds the right column
+                    const float o0 = __shfl_xor(l2[bb][0], 32), o1 = __shfl_xor(l2[bb][1], 32);
+                    l3[bb] = pool4_v(l2[bb][0], o0, l2[bb][1], o1);
+                }
+            } else {
+                // band: line j = row g4 x cols 8 j + 4 arow + t; level 1 rows y1 = 0..1, cols
+                // 4 j + 2 arow + c (l1[bb][2 y1 + jl][c]); level 2 col 2 j + arow
+#pragma unroll
+                for (int jl = 0; jl < 2; ++jl)
+#pragma unroll
+                    for (int y1 = 0; y1 < 2; ++y1)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c)
+                            l1[bb][2 * y1 + jl][c] = pool4_v(v[jl][2 * y1][2 * c], v[jl][2 * y1][2 * c + 1],
+                                                           v[jl][2 * y1 + 1][2 * c], v[jl][2 * y1 + 1][2 * c + 1]);
+                if (L >= 3) {   // level 2: col 2 (2 bb + jl) + arow (stored per i below)
+#pragma unroll
+                    for (int jl = 0; jl < 2; ++jl)
+                        l2[bb][jl] = pool4_v(l1[bb][jl][0], l1[bb][jl][1], l1[bb][2 + jl][0], l1[bb][2 + jl][1]);
+                }
+            }
+        }
+        if (L < 2) continue;
+        if (L >= 3) {
+            // level 2: one 16-byte row piece per lane.  Regular: the n-tile's 2 x 4 pixels, lane
+            // acol row 0, lane acol + 32 row 1, cols {2 bb, 2 bb + 1} = (l2[bb][0] | l2[bb][1]) after
+            // swapping row 1 of the arow-0 lanes with row 0 of the arow-1 lanes.  Band: the 1 x 8
+            // pixels, lane acol cols 0-3, lane acol + 32 cols 4-7 (swap bb = 1 of the arow-0 lanes
+            // with bb = 0 of the arow-1 lanes)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (!tc.band) swap32(l2[k][0], l2[k][1]);
+                else swap32(l2[0][k], l2[1][k]);
+            }
+            const floatx4 row2 = tc.band ? floatx4{l2[0][0], l2[1][0], l2[0][1], l2[1][1]}
+                                         : floatx4{l2[0][0], l2[0][1], l2[1][0], l2[1][1]};
+            store_px(r2, 2, ql + acol, (tc.ty0 >> 2) + (tc.band ? 0 : arow), (tc.tx0 >> 2) + (tc.band ? 4 * arow : 0), row2);
+            if (L >= 4 && !tc.band)   // level 3: the n-tile's 1 x 2 pixels, from the arow-0 lanes
+                store_px(r3, 3, arow ? nq : ql + acol, tc.ty0 >> 3, tc.tx0 >> 3, floatx2{l3[0], l3[1]});
+        }
+        // level 1 (regular: the n-tile's 4 x 8 level-1 pixels = one tile line; band: rows 0-1 of
+        // two tile lines u = 0, 1, whose segment 0 the lanes acol / acol + 32 store)
+        char* const xp = xw;
+        if (!tc.band) {
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+                for (int y1 = 0; y1 < 4; ++y1)
+                    *reinterpret_cast<floatx2*>(xp + wo + 32 * y1 + 4 * (4 * bb + 2 * arow)) = floatx2{l1[bb][y1][0], l1[bb][y1][1]};
+        } else {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int y1 = 0; y1 < 2; ++y1)
+#pragma unroll
+                    for (int jl = 0; jl < 2; ++jl)
+                        *reinterpret_cast<floatx2*>(xp + wo + 64 * u + 32 * y1 + 4 * (4 * jl + 2 * arow)) =
+                            floatx2{l1[u][2 * y1 + jl][0], l1[u][2 * y1 + jl][1]};
+        }
+        const int r1t = tc.ty0 >> 3;                                   // level-1 tile row
+        const int c1t = (tc.tx0 >> 4) + (tc.band ? arow : 0);          // level-1 tile col
+        store_lines(xp, r1, P.lsz[1], ql, ((r1t * P.lntx[1] + c1t) * kTile) * 4 + (tc.band ? 0 : 64 * arow),
+                    r1t < P.lnty[1] && c1t < P.lntx[1]);
+    }
+}
+
 // NK: K chunks known at compile time (16: D = 256, the E-RAFT feature width) -- the K loop is then
 // fully unrolled, which lets hipcc count the in-flight query loads exactly (in the rolled loop it
 // drains them at the loop header); 0 = any D.
@@ -223,7 +441,6 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
     float* fst = reinterpret_cast<float*>(ext + 128);           // 2^ext when |ext| <= 63
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int acol = lane & 31, arow = lane >> 5;
     int b, qt, nt;
     decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
     const NTile tc = ntile_of(P, nt);
@@ -443,214 +660,7 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
         for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
 
     // ---------------- epilogue (per wave, from registers) ----------------
-    // Line segments through a wave-private LDS transpose (no barrier: a wave's LDS accesses are
-    // processed in order): the lane writes its 16-byte pieces into the line image of its query
-    // (32 queries x 144 B: conflict-free ds_write_b128 and ds_read_b128), then reads back piece m
-    // of segment arow of query 4k + s, so the 4 lanes of a quad store 64 contiguous bytes and
-    // lanes acol, acol + 32 the two halves of one line.
-    // four regions per wave (one per level-0 line of a tile row; the level-1 line reuses region
-    // 0): no line waits for the previous line's read-back before writing
-    char* const xw = smem + wave * (4 * 32 * XS);
-    const int m4 = lane & 3, k4 = acol >> 2;
-    const int wo = acol * XS, ro = (4 * k4) * XS + 64 * arow + 16 * m4;
-    const int L = P.fused_levels;
-    const int64_t rows0 = (int64_t)b * P.q_count + q0;   // the block's first query image
-    const int nq = min(SQ, P.q_count - q0);
-    // per-level descriptors over the block's query images (range check = query bound); levels 2-3
-    // (interleaved): over the 64-row groups the block's rows touch, from group g0 = rows0 / 64
-    const int64_t g0 = rows0 >> 6;
-    auto rsrc_of = [&](int lv) {
-        if (lv >= 2)
-            return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + g0 * kGroup * P.lsz[lv], 0,
-                                                     (int)((((rows0 + nq - 1) >> 6) - g0 + 1) * kGroup * P.lsz[lv] * 4),
-                                                     0x00020000);
-        return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + rows0 * P.lsz[lv], 0, (int)(nq * P.lsz[lv] * 4), 0x00020000);
-    };
-    // read the transposed segments back and store them: line byte offset lo (+ the query image)
-    auto store_lines = [&](const char* xp, __amdgpu_buffer_rsrc_t rs, int64_t lsz, int ql, int lo, bool ok) {
-        floatx4 pc[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) pc[s] = *reinterpret_cast<const floatx4*>(xp + ro + s * XS);
-        const int base = (int)((ql + 4 * k4) * lsz * 4) + lo + 16 * m4;
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, pc[s]), rs,
-                                                   ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_L01);
-    };
-    // One block row (r, c .. c + N - 1), N = the block width, of level 2 or 3 (interleaved) for
-    // block-local query qloc: lanes on consecutive queries write consecutive 4N-byte pieces, so a
-    // store instruction covers whole lines, which leave non-temporally like levels 0-1 (A/B: 656
-    // vs 685 us with plain stores, which park the lines in L2).  Queries past the block and
-    // blocks outside the level are dropped (padding cells of a block are written, never read).
-    auto store_px = [&](__amdgpu_buffer_rsrc_t rs, int lv, int qloc, int r, int c, auto val) {
-        constexpr int N = sizeof(val) / 4;
-        const int sy = ilv_sy(lv), sx = ilv_sx(lv);
-        const int by = r >> sy, bx = c >> sx;
-        const bool in = qloc < nq && by < P.lnty[lv] && bx < -P.lntx[lv];
-        const int64_t R = rows0 + qloc;
-        const int off = (int)((((R >> 6) - g0) * kGroup * P.lsz[lv] +
-                               ((int64_t)(by * -P.lntx[lv] + bx) * kGroup + (R & (kGroup - 1))) * (1 << (sy + sx)) +
-                               ((r & ((1 << sy) - 1)) << sx)) * 4);
-        if constexpr (N == 4)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, ST_L01);
-        else
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, val), rs, in ? off : SOOB, 0, ST_L01);
-    };
-    // Scaling: x = acc 2^(nqe + ext) (/ sqrt(D) when that is no power of two).  Where every
-    // exponent of the wave's queries and of the panel's targets lies in [-63, 63], the 2^nqe 2^ext
-    // product is a normal power of two and one multiply by it rounds exactly as ldexpf does: two
-    // packed multiplies per element pair instead of an add, a negate and an ldexp per element.
-    bool fast_scale;
-    {
-        bool ok = ext[lane] >= -63 && ext[lane] <= 63 && ext[lane + 64] >= -63 && ext[lane + 64] <= 63;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int n = -(exq[wave * 64 + 32 * i + acol] + (MUL ? P.scale_shift : 0));
-            ok = ok && n >= -63 && n <= 63;
-        }
-        fast_scale = __all(ok);
-    }
-    const __amdgpu_buffer_rsrc_t r0 = rsrc_of(0);
-    const __amdgpu_buffer_rsrc_t r1 = rsrc_of(L > 1 ? 1 : 0);
-    const __amdgpu_buffer_rsrc_t r2 = rsrc_of(L > 2 ? 2 : 0);
-    const __amdgpu_buffer_rsrc_t r3 = rsrc_of(L > 3 ? 3 : 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int ql = wave * 64 + 32 * i;          // first block-local query of this tile row
-        const int nqe = -(exq[ql + acol] + (MUL ? P.scale_shift : 0));
-        // level-1 values of the lane's query: [block bb][row][col pair] (band: [half][2 y1 + jl]);
-        // level 2: [bb][row r] (band: [bb][jl]); level 3: [bb]
-        float l1[2][4][2], l2[2][2], l3[2];
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-            // scaled values of lines j = 2 bb + jl, [jl][g4][t]; target exponents
-            // ext[32 j + 8 g4 + 4 arow + t]
-            float v[2][4][4];
-            if (fast_scale) {
-                const float sq = exp2i(nqe);
-#pragma unroll
-                for (int jl = 0; jl < 2; ++jl) {
-                    const int j = 2 * bb + jl;
-#pragma unroll
-                    for (int g4 = 0; g4 < 4; ++g4) {
-                        const floatx4 s4 = *reinterpret_cast<const floatx4*>(fst + 32 * j + 8 * g4 + 4 * arow);
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const float x = __fmul_rn(acc[i][j][4 * g4 + t], __fmul_rn(sq, s4[t]));
-                            v[jl][g4][t] = MUL ? x : __fdiv_rn(x, P.scale);
-                        }
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int jl = 0; jl < 2; ++jl) {
-                    const int j = 2 * bb + jl;
-#pragma unroll
-                    for (int g4 = 0; g4 < 4; ++g4) {
-                        const int4 e4 = *reinterpret_cast<const int4*>(ext + 32 * j + 8 * g4 + 4 * arow);
-                        const int e[4] = {e4.x, e4.y, e4.z, e4.w};
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const float x = ldexpf(acc[i][j][4 * g4 + t], nqe + e[t]);
-                            v[jl][g4][t] = MUL ? x : __fdiv_rn(x, P.scale);
-                        }
-                    }
-                }
-            }
-            // level 0: line j = rows g4 x this lane's 4 columns
-#pragma unroll
-            for (int jl = 0; jl < 2; ++jl) {
-                const int j = 2 * bb + jl;
-                char* const xp = xw + j * (32 * XS);
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4)
-                    *reinterpret_cast<floatx4*>(xp + wo + 32 * g4 + 16 * arow) =
-                        floatx4{v[jl][g4][0], v[jl][g4][1], v[jl][g4][2], v[jl][g4][3]};
-                const int tr = (tc.ty0 >> 2) + (tc.band ? 0 : (j & 1));
-                const int tcl = (tc.tx0 >> 3) + (tc.band ? j : (j >> 1));
-                store_lines(xp, r0, P.lsz[0], ql, ((tr * P.lntx[0] + tcl) * kTile) * 4 + 64 * arow,
-                            tr < P.lnty[0] && tcl < P.lntx[0]);
-            }
-            if (L < 2) continue;
-            if (!tc.band) {
-                // regular: line j = rows 4 jl + g4 of 8 x 8 block bb; level 1 rows y1 = 0..3, cols
-                // 4 bb + 2 arow + c; level 2 rows r, col 2 bb + arow; level 3 needs lane acol + 32
-#pragma unroll
-                for (int y1 = 0; y1 < 4; ++y1)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const int jl = y1 >> 1, g = 2 * (y1 & 1);
-                        l1[bb][y1][c] = pool4_v(v[jl][g][2 * c], v[jl][g][2 * c + 1], v[jl][g + 1][2 * c],
-                                              v[jl][g + 1][2 * c + 1]);
-                    }
-                if (L >= 3) {   // level 2: rows r, col 2 bb + arow (stored per i below)
-#pragma unroll
-                    for (int r = 0; r < 2; ++r)
-                        l2[bb][r] = pool4_v(l1[bb][2 * r][0], l1[bb][2 * r][1], l1[bb][2 * r + 1][0], l1[bb][2 * r + 1][1]);
-                    // level 3, the 8 x 8 pool: lane acol + 32 holds the right column
-                    const float o0 = __shfl_xor(l2[bb][0], 32), o1 = __shfl_xor(l2[bb][1], 32);
-                    l3[bb] = pool4_v(l2[bb][0], o0, l2[bb][1], o1);
-                }
-            } else {
-                // band: line j = row g4 x cols 8 j + 4 arow + t; level 1 rows y1 = 0..1, cols
-                // 4 j + 2 arow + c (l1[bb][2 y1 + jl][c]); level 2 col 2 j + arow
-#pragma unroll
-                for (int jl = 0; jl < 2; ++jl)
-#pragma unroll
-                    for (int y1 = 0; y1 < 2; ++y1)
-#pragma unroll
-                        for (int c = 0; c < 2; ++c)
-                            l1[bb][2 * y1 + jl][c] = pool4_v(v[jl][2 * y1][2 * c], v[jl][2 * y1][2 * c + 1],
-                                                           v[jl][2 * y1 + 1][2 * c], v[jl][2 * y1 + 1][2 * c + 1]);
-                if (L >= 3) {   // level 2: col 2 (2 bb + jl) + arow (stored per i below)
-#pragma unroll
-                    for (int jl = 0; jl < 2; ++jl)
-                        l2[bb][jl] = pool4_v(l1[bb][jl][0], l1[bb][jl][1], l1[bb][2 + jl][0], l1[bb][2 + jl][1]);
-                }
-            }
-        }
-        if (L < 2) continue;
-        if (L >= 3) {
-            // level 2: one 16-byte row piece per lane.  Regular: the n-tile's 2 x 4 pixels, lane
-            // acol row 0, lane acol + 32 row 1, cols {2 bb, 2 bb + 1} = (l2[bb][0] | l2[bb][1]) after
-            // swapping row 1 of the arow-0 lanes with row 0 of the arow-1 lanes.  Band: the 1 x 8
-            // pixels, lane acol cols 0-3, lane acol + 32 cols 4-7 (swap bb = 1 of the arow-0 lanes
-            // with bb = 0 of the arow-1 lanes)
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                if (!tc.band) swap32(l2[k][0], l2[k][1]);
-                else swap32(l2[0][k], l2[1][k]);
-            }
-            const floatx4 row2 = tc.band ? floatx4{l2[0][0], l2[1][0], l2[0][1], l2[1][1]}
-                                         : floatx4{l2[0][0], l2[0][1], l2[1][0], l2[1][1]};
-            store_px(r2, 2, ql + acol, (tc.ty0 >> 2) + (tc.band ? 0 : arow), (tc.tx0 >> 2) + (tc.band ? 4 * arow : 0), row2);
-            if (L >= 4 && !tc.band)   // level 3: the n-tile's 1 x 2 pixels, from the arow-0 lanes
-                store_px(r3, 3, arow ? nq : ql + acol, tc.ty0 >> 3, tc.tx0 >> 3, floatx2{l3[0], l3[1]});
-        }
-        // level 1 (regular: the n-tile's 4 x 8 level-1 pixels = one tile line; band: rows 0-1 of
-        // two tile lines u = 0, 1, whose segment 0 the lanes acol / acol + 32 store)
-        char* const xp = xw;
-        if (!tc.band) {
-#pragma unroll
-            for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-                for (int y1 = 0; y1 < 4; ++y1)
-                    *reinterpret_cast<floatx2*>(xp + wo + 32 * y1 + 4 * (4 * bb + 2 * arow)) = floatx2{l1[bb][y1][0], l1[bb][y1][1]};
-        } else {
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int y1 = 0; y1 < 2; ++y1)
-#pragma unroll
-                    for (int jl = 0; jl < 2; ++jl)
-                        *reinterpret_cast<floatx2*>(xp + wo + 64 * u + 32 * y1 + 4 * (4 * jl + 2 * arow)) =
-                            floatx2{l1[u][2 * y1 + jl][0], l1[u][2 * y1 + jl][1]};
-        }
-        const int r1t = tc.ty0 >> 3;                                   // level-1 tile row
-        const int c1t = (tc.tx0 >> 4) + (tc.band ? arow : 0);          // level-1 tile col
-        store_lines(xp, r1, P.lsz[1], ql, ((r1t * P.lntx[1] + c1t) * kTile) * 4 + (tc.band ? 0 : 64 * arow),
-                    r1t < P.lnty[1] && c1t < P.lntx[1]);
-    }
+    split_epilogue<MUL>(P, acc, smem + wave * (4 * 32 * XS), wave * 64, exq, ext, fst, tc, b, q0, lane);
 }
 
 // Split-mode operand pass: per pixel, ex = 15 - E with max_d |x| = f 2^E, f in [0.5, 1) (so the
