@@ -689,22 +689,43 @@ template <bool ISB>
 __device__ __forceinline__ void pack_body(const float* __restrict__ x, const BuildParams& P, int* __restrict__ ex,
                                           char* __restrict__ pack) {
     __shared__ float red[4][64];
-    const int b = blockIdx.y, tile = blockIdx.x >> 1;
+    const int b = blockIdx.y;
+    int tile = blockIdx.x >> 1;
     int pos = (blockIdx.x & 1) * 64 + (threadIdx.x & 63);   // panel position of this lane's pixel
     const int qtr = threadIdx.x >> 6, D = P.D, dc = (D + 15) / 16;
     const int64_t N = ISB ? (int64_t)P.H * P.W : (int64_t)P.q_count;
     int64_t pix = -1;
+    bool live = true;   // the lane owns a panel position (it writes its zeros too)
     if (!ISB) {
         const int64_t p = (int64_t)tile * 128 + pos;
         if (p < P.q_count) pix = p;
     } else {
-        // lanes in raster order over half the n-tile (16 consecutive pixels per row: 64-byte
-        // reads), each at its panel position (split_target inverted)
-        const NTile n = ntile_of(P, tile);
-        const int h = blockIdx.x & 1, l = threadIdx.x & 63;
-        const int y = n.band ? l >> 4 : 4 * h + (l >> 4), x = n.band ? 16 * h + (l & 15) : l & 15;
-        pos = n.band ? 32 * (x >> 3) + 8 * y + (x & 7) : 64 * (x >> 3) + 32 * (y >> 2) + 8 * (y & 3) + (x & 7);
-        if (n.ty0 + y < P.H && n.tx0 + x < P.W) pix = (int64_t)(n.ty0 + y) * P.W + n.tx0 + x;
+        // lanes on 2 rows x 32 consecutive pixels (whole 128-byte lines of fmap2: an L2 miss
+        // fetches the whole line, so 16-pixel row pieces read every line twice): regular blocks
+        // cover rows 2 r4, 2 r4 + 1 of a pair of horizontally adjacent 8 x 16 n-tiles, band blocks
+        // rows 2 h, 2 h + 1 of one 4 x 32 band tile; each lane goes to its n-tile's panel
+        // position (split_target inverted)
+        const int l = threadIdx.x & 63, npair = (P.n_ntx + 1) / 2, nreg_blk = 4 * (P.n_reg / P.n_ntx) * npair;
+        int y, x;
+        bool ok;
+        if ((int)blockIdx.x < nreg_blk) {
+            const int r4 = blockIdx.x & 3, pr = blockIdx.x >> 2, trow = pr / npair, col = 2 * (pr - trow * npair) + (l >> 4 & 1);
+            ok = col < P.n_ntx;
+            tile = trow * P.n_ntx + (ok ? col : 0);
+            y = 2 * r4 + (l >> 5);
+            x = l & 15;
+            pos = 64 * (x >> 3) + 32 * (y >> 2) + 8 * (y & 3) + (x & 7);
+        } else {
+            const int bb = blockIdx.x - nreg_blk;
+            tile = P.n_reg + (bb >> 1);
+            ok = tile < P.n_nt;
+            y = 2 * (bb & 1) + (l >> 5);
+            x = l & 31;
+            pos = 32 * (x >> 3) + 8 * y + (x & 7);
+        }
+        const NTile n = ntile_of(P, ok ? tile : 0);
+        live = ok;
+        if (ok && n.ty0 + y < P.H && n.tx0 + x < P.W) pix = (int64_t)(n.ty0 + y) * P.W + n.tx0 + x;
     }
     const float* px = x + (int64_t)b * D * N + (pix < 0 ? 0 : pix);
     constexpr int CPT = 4;
@@ -747,6 +768,7 @@ __device__ __forceinline__ void pack_body(const float* __restrict__ x, const Bui
         *reinterpret_cast<halfx8*>(p + 1024) = l0;
         *reinterpret_cast<halfx8*>(p + 1536) = l1;
     };
+    if (!live) return;   // (after the block's only barrier)
     if (regs) {
 #pragma unroll
         for (int i = 0; i < CPT; ++i)
@@ -771,7 +793,7 @@ __device__ __forceinline__ void pack_body(const float* __restrict__ x, const Bui
 __global__ __launch_bounds__(256) void pack_both_kernel(BuildParams P) {
     if (blockIdx.z == 0) {
         if ((int)blockIdx.x < 2 * P.n_mt) pack_body<false>(P.f1, P, P.ex1, const_cast<char*>(P.pk1));
-    } else if ((int)blockIdx.x < 2 * P.n_nt) {
+    } else if ((int)blockIdx.x < 4 * (P.n_reg / P.n_ntx) * ((P.n_ntx + 1) / 2) + 2 * (P.n_nt - P.n_reg)) {
         pack_body<true>(P.f2, P, P.ex2, const_cast<char*>(P.pk2));
     }
 }
@@ -1255,7 +1277,8 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
         P.ex2 = reinterpret_cast<int*>(P.ws + w.ex2);
         P.pk1 = P.ws + w.pk1;
         P.pk2 = P.ws + w.pk2;
-        const int nx = 2 * (P.n_mt > P.n_nt ? P.n_mt : P.n_nt);
+        const int nx2 = 4 * (P.n_reg / P.n_ntx) * ((P.n_ntx + 1) / 2) + 2 * (P.n_nt - P.n_reg);   // fmap2 blocks
+        const int nx = 2 * P.n_mt > nx2 ? 2 * P.n_mt : nx2;
         if (stages & 1) hipLaunchKernelGGL(pack_both_kernel, dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
         if (!(stages & 2)) {
             const hipError_t e = hipGetLastError();
