@@ -23,9 +23,9 @@ __host__ __device__ __forceinline__ int tiled_off(int y, int x, int ntx) {
 __host__ __device__ __forceinline__ int pad_h(int h) { return (h + kTileH - 1) & ~(kTileH - 1); }
 __host__ __device__ __forceinline__ int pad_w(int w) { return (w + kTileW - 1) & ~(kTileW - 1); }
 
-// Levels >= 2 whose tile padding would exceed half the image (DSEC level 3: 7 x 10 -> 8 x 16) are
-// stored compact row-major instead: the window covers most of such an image, so the padding would
-// only add lines to every lookup's read footprint (tools/lookup_lab.hip: -5% lookup time).
+// Levels >= 4 (levels 2-3 are interleaved, below) whose tile padding would exceed half the image
+// are stored compact row-major instead: the window covers most of such an image, so the padding
+// would only add lines to every lookup's read footprint.
 __host__ __device__ __forceinline__ bool level_compact(int level, int h, int w) {
     return level >= 2 && 2 * pad_h(h) * pad_w(w) > 3 * h * w;
 }
