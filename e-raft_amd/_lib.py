@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 MAX_LEVELS = 16
 
 ECORR_OK = 0

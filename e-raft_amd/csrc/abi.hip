@@ -26,7 +26,7 @@ int pyramid_geometry(int64_t rows, int H, int W, int levels, PyrGeom* g) {
         g->h[i] = hh;
         g->w[i] = ww;
         int64_t nrows = rows;
-        if (i == 2 || i == 3) {   // interleaved (ecorr_device.h pix_off): blocks of (8 >> i) x (16 >> i)
+        if (i >= 1 && i <= 3) {   // interleaved (ecorr_device.h pix_off): 2 x 4 / 2 x 4 / 1 x 2 blocks
             const int bh = 1 << ilv_sy(i), bw = 1 << ilv_sx(i);
             const int nby = (hh + bh - 1) / bh, nbx = (ww + bw - 1) / bw;
             g->ntx[i] = -nbx;

@@ -235,7 +235,7 @@ __device__ __forceinline__ void split_epilogue(const BuildParams& P, floatx16 (&
     // (interleaved): over the 64-row groups the block's rows touch, from group g0 = rows0 / 64
     const int64_t g0 = rows0 >> 6;
     auto rsrc_of = [&](int lv) {
-        if (lv >= 2)
+        if (lv >= 1)
             return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + g0 * kGroup * P.lsz[lv], 0,
                                                      (int)((((rows0 + nq - 1) >> 6) - g0 + 1) * kGroup * P.lsz[lv] * 4),
                                                      0x00020000);
@@ -402,29 +402,28 @@ __device__ __forceinline__ void split_epilogue(const BuildParams& P, floatx16 (&
             if (L >= 4 && !tc.band)   // level 3: the n-tile's 1 x 2 pixels, from the arow-0 lanes
                 store_px(r3, 3, arow ? nq : ql + acol, tc.ty0 >> 3, tc.tx0 >> 3, floatx2{l3[0], l3[1]});
         }
-        // level 1 (regular: the n-tile's 4 x 8 level-1 pixels = one tile line; band: rows 0-1 of
-        // two tile lines u = 0, 1, whose segment 0 the lanes acol / acol + 32 store)
-        char* const xp = xw;
-        if (!tc.band) {
+        // level 1 (interleaved 2 x 4 blocks): the lane holds cols 2 arow, 2 arow + 1 of each block
+        // row; one swap of rows between the arow halves leaves lane acol with row 0 and lane
+        // acol + 32 with row 1 of the block, each a 16-byte piece (as level 2).  Regular: blocks
+        // (r, bb) = level-1 rows ty0/2 + 2r .. +1, cols tx0/2 + 4 bb .. +3 (l1[bb][y1][c], y1 = 2r,
+        // 2r + 1); band: blocks j = 2 bb + jl = rows ty0/2 .. +1, cols tx0/2 + 4j .. +3
+        // (l1[bb][2 y1 + jl][c])
 #pragma unroll
-            for (int bb = 0; bb < 2; ++bb)
+        for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-                for (int y1 = 0; y1 < 4; ++y1)
-                    *reinterpret_cast<floatx2*>(xp + wo + 32 * y1 + 4 * (4 * bb + 2 * arow)) = floatx2{l1[bb][y1][0], l1[bb][y1][1]};
-        } else {
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int y1 = 0; y1 < 2; ++y1)
-#pragma unroll
-                    for (int jl = 0; jl < 2; ++jl)
-                        *reinterpret_cast<floatx2*>(xp + wo + 64 * u + 32 * y1 + 4 * (4 * jl + 2 * arow)) =
-                            floatx2{l1[u][2 * y1 + jl][0], l1[u][2 * y1 + jl][1]};
-        }
-        const int r1t = tc.ty0 >> 3;                                   // level-1 tile row
-        const int c1t = (tc.tx0 >> 4) + (tc.band ? arow : 0);          // level-1 tile col
-        store_lines(xp, r1, P.lsz[1], ql, ((r1t * P.lntx[1] + c1t) * kTile) * 4 + (tc.band ? 0 : 64 * arow),
-                    r1t < P.lnty[1] && c1t < P.lntx[1]);
+            for (int r = 0; r < 2; ++r) {
+                float x0, x1, y0, y1;
+                if (!tc.band) {
+                    x0 = l1[bb][2 * r][0], x1 = l1[bb][2 * r][1], y0 = l1[bb][2 * r + 1][0], y1 = l1[bb][2 * r + 1][1];
+                } else {
+                    x0 = l1[bb][r][0], x1 = l1[bb][r][1], y0 = l1[bb][2 + r][0], y1 = l1[bb][2 + r][1];
+                }
+                swap32(x0, y0);
+                swap32(x1, y1);
+                const int yb = (tc.ty0 >> 1) + (tc.band ? 0 : 2 * r) + arow;
+                const int xb = (tc.tx0 >> 1) + (tc.band ? 4 * (2 * bb + r) : 4 * bb);
+                store_px(r1, 1, ql + acol, yb, xb, floatx4{x0, x1, y0, y1});
+            }
     }
 }
 
@@ -885,18 +884,13 @@ __device__ __forceinline__ void epilogue(const BuildParams& P, const TileCoord& 
         S3[m * 2 + blk] = l3;
     }
     __syncthreads();
-    {   // level 1: tile (ty0/8, tx0/16), 8 float4 per query
-        const int tr = tc.ty0 / 8, tcc = tc.tx0 / 16;
-        if (tr < P.lnty[1] && tcc < P.lntx[1]) {
-            float* base = P.lvl[1] + (tr * P.lntx[1] + tcc) * kTile;
+    {   // level 1 (interleaved): rows ty0/2 .. +3, cols tx0/2 .. +7, 8 float4 block-row pieces per query
 #pragma unroll
-            for (int s = 0; s < (MR * 8) / NT; ++s) {
-                const int idx = tid + NT * s;
-                const int mm = idx >> 3, j = idx & 7;
-                if (mm < mvalid)
-                    st_nt(reinterpret_cast<floatx4*>(base + (row0 + mm) * P.lsz[1] + 4 * j),
-                          *reinterpret_cast<const floatx4*>(S1 + mm * P1S + 4 * j));
-            }
+        for (int s = 0; s < (MR * 8) / NT; ++s) {
+            const int idx = tid + NT * s;
+            const int mm = idx >> 3, j = idx & 7;
+            float* p = mm < mvalid ? level_px(P, 1, row0 + mm, tc.ty0 / 2 + (j >> 1), tc.tx0 / 2 + 4 * (j & 1)) : nullptr;
+            if (p) st_nt(reinterpret_cast<floatx4*>(p), *reinterpret_cast<const floatx4*>(S1 + mm * P1S + 4 * j));
         }
     }
     if (P.fused_levels >= 3 && tid < 2 * MR) {   // level 2: rows ty0/4 + {0,1}, cols tx0/4 .. +3
@@ -980,19 +974,15 @@ __device__ __forceinline__ void epilogue_band(const BuildParams& P, const TileCo
         }
     }
     __syncthreads();
-    {   // level 1: rows ty0/2 .. +1 (in-tile rows 0-1 of tile row ty0/8), tile cols tx0/16 .. +1
-        const int tr = tc.ty0 / 8, tc0 = tc.tx0 / 16;
-        if (tr < P.lnty[1]) {
+    {   // level 1 (interleaved): rows ty0/2 .. +1, cols tx0/2 .. +15, 8 float4 block-row pieces per query
 #pragma unroll
-            for (int s = 0; s < (MR * 8 + NT - 1) / NT; ++s) {
-                const int idx = tid + NT * s;
-                const int mm = idx >> 3, t = idx & 7;
-                const int y = t >> 2, tcl = (t >> 1) & 1, hf = t & 1;
-                if (mm < mvalid && tc0 + tcl < P.lntx[1])
-                    st_nt(reinterpret_cast<floatx4*>(P.lvl[1] + (row0 + mm) * P.lsz[1] +
-                                                     (tr * P.lntx[1] + tc0 + tcl) * kTile + y * 8 + hf * 4),
-                          *reinterpret_cast<const floatx4*>(S1 + mm * P1S + y * 16 + tcl * 8 + hf * 4));
-            }
+        for (int s = 0; s < (MR * 8 + NT - 1) / NT; ++s) {
+            const int idx = tid + NT * s;
+            const int mm = idx >> 3, t = idx & 7;
+            const int y = t >> 2, tcl = (t >> 1) & 1, hf = t & 1;
+            float* p = mm < mvalid ? level_px(P, 1, row0 + mm, tc.ty0 / 2 + y, tc.tx0 / 2 + tcl * 8 + hf * 4) : nullptr;
+            if (p)
+                st_nt(reinterpret_cast<floatx4*>(p), *reinterpret_cast<const floatx4*>(S1 + mm * P1S + y * 16 + tcl * 8 + hf * 4));
         }
     }
     if (P.fused_levels >= 3 && tid < 2 * MR) {   // level 2: row ty0/4, cols tx0/4 .. +7

@@ -36,15 +36,15 @@ __host__ __device__ __forceinline__ int level_off(int y, int x, int ntx, int w) 
     return ntx > 0 ? tiled_off(y, x, ntx) : y * w + x;
 }
 
-// Levels 2 and 3 are stored interleaved (ntx = -nbx < 0): query rows in groups of kGroup = 64, and a
-// group holds, for each (8 >> lv) x (16 >> lv) block of the level image -- what one 8 x 16 target
-// block of level 0 pools to -- that block of its 64 rows back to back: [group][block][row][bh][bw],
-// blocks row-major (nbx per block row).  One build tile then writes each level-2/3 block of its
-// 256 query rows as whole lines (the per-row pieces are 32 / 8 bytes), and the lookup reads a
-// window's blocks with lines shared by adjacent queries.
+// Levels 1-3 are stored interleaved (ntx = -nbx < 0): query rows in groups of kGroup = 64, and a
+// group holds, for each bh x bw block of the level image (2 x 4 at levels 1 and 2, 1 x 2 at level
+// 3: what one 8 x 16 target block of level 0 pools to at levels 2 and 3), that block of its 64 rows
+// back to back: [group][block][row][bh][bw], blocks row-major (nbx per block row).  One build tile
+// then writes each block of its 256 query rows as whole lines (the per-row pieces are 32 / 8
+// bytes), and the lookup reads a window's blocks with lines shared by adjacent queries.
 constexpr int kGroup = ECORR_ROW_GROUP;
-__host__ __device__ __forceinline__ int ilv_sy(int lv) { return 3 - lv; }   // log2 block height
-__host__ __device__ __forceinline__ int ilv_sx(int lv) { return 4 - lv; }   // log2 block width
+__host__ __device__ __forceinline__ int ilv_sy(int lv) { return lv == 3 ? 0 : 1; }   // log2 block height
+__host__ __device__ __forceinline__ int ilv_sx(int lv) { return lv == 3 ? 1 : 2; }   // log2 block width
 
 // Float offset of pixel (y, x) of query row R (0 .. B*q_count - 1) from the level's base, any
 // format; sz = floats per query image (an interleaved group spans kGroup * sz floats).

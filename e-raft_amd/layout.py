@@ -1,8 +1,8 @@
-"""Pyramid storage (include/ecorr.h).  Each query image of levels 0-1 (and >= 4) is stored as
+"""Pyramid storage (include/ecorr.h).  Each query image of level 0 (and >= 4) is stored as
 row-major 4 x 8-float tiles (128 bytes, one L2 line) or, for small levels >= 4 where tile padding
-would exceed half the image, compact row-major; levels 2 and 3 are interleaved: query rows in
-groups of 64, each group storing every (8 >> i) x (16 >> i) block of the level for its 64 rows back
-to back.  `formats` asks libecorr which (ntx = tiles per tile row, 0 = compact, -nbx =
+would exceed half the image, compact row-major; levels 1-3 are interleaved: query rows in groups
+of 64, each group storing every 2 x 4 (levels 1-2) / 1 x 2 (level 3) block of the level for its 64
+rows back to back.  `formats` asks libecorr which (ntx = tiles per tile row, 0 = compact, -nbx =
 interleaved with nbx blocks per block row).  `untile` turns a level back into the reference's
 corr_pyramid shape [rows, 1, h, w] (nothing on the E-RAFT path reads corr_pyramid,
 corr.py:16-27); `tile` and `pack` are the inverse, used to feed externally produced pyramids
@@ -24,9 +24,9 @@ GROUP = 64   # query rows per interleave group (ecorr_device.h kGroup)
 
 
 def block_shape(level):
-    """(bh, bw) of an interleaved level's blocks: what one 8 x 16 level-0 target block pools to."""
-    assert level in (2, 3), level
-    return 8 >> level, 16 >> level
+    """(bh, bw) of an interleaved level's blocks (include/ecorr.h): 2 x 4 at levels 1-2, 1 x 2 at 3."""
+    assert level in (1, 2, 3), level
+    return (1, 2) if level == 3 else (2, 4)
 
 
 def formats(H, W, levels):

@@ -13,13 +13,14 @@
  * aligned); level i holds rows = B * q_count query images of h_i x w_i (h_0 = H, w_0 = W,
  * h_{i+1} = h_i / 2, w_{i+1} = w_i / 2, floor -- the shapes of the reference's corr_pyramid[i],
  * corr.py:16-27).  Each level is stored in one of three formats (ecorr_pyramid_formats):
- *   tiled (ntx_i > 0; levels 0, 1 and >= 4): row-major ECORR_TILE_H x ECORR_TILE_W tiles of 32
+ *   tiled (ntx_i > 0; levels 0 and >= 4): row-major ECORR_TILE_H x ECORR_TILE_W tiles of 32
  *     floats (128 bytes, one L2 line); image r starts at off_i + r * hp_i * wp_i,
  *     hp_i = roundup(h_i, 4), wp_i = roundup(w_i, 8) = 8 * ntx_i, and pixel (y, x) sits at
  *     ((y / 4) * ntx_i + x / 8) * 32 + (y % 4) * 8 + x % 8.  A radius-4 window then touches ~7
  *     lines per level instead of ~13 with row-major images; padding cells are never read.
- *   interleaved (ntx_i = -nbx < 0; levels 2 and 3): blocks of bh x bw = (8 >> i) x (16 >> i)
- *     pixels (what one 8 x 16 block of level 0 pools to), nby = ceil(h_i / bh) by nbx =
+ *   interleaved (ntx_i = -nbx < 0; levels 1, 2 and 3): blocks of bh x bw = 2 x 4 (levels 1 and 2)
+ *     or 1 x 2 (level 3) pixels (at levels 2 and 3 what one 8 x 16 block of level 0 pools to),
+ *     nby = ceil(h_i / bh) by nbx =
  *     ceil(w_i / bw) of them per image, sz = nby * nbx * bh * bw floats per image; the rows are
  *     taken in groups of ECORR_ROW_GROUP = 64 (the level holds roundup(rows, 64) * sz floats) and
  *     pixel (y, x) of row r sits at (r / 64) * 64 * sz + (((y / bh) * nbx + x / bw) * 64 + r % 64)
@@ -42,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 12
+#define ECORR_ABI_VERSION 13
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8

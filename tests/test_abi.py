@@ -61,22 +61,23 @@ def test_layout_matches_reference_shapes(ea):
     from eraft_amd import _lib
     h, w, off = _lib.layout(16 * 4800, 60, 80, 4)
     assert (h, w) == ([60, 30, 15, 7], [80, 40, 20, 10])
-    # levels 0-1 tiled (each image padded to 4 x 8 tiles: 60x80, 32x40); levels 2-3 interleaved in
-    # 2 x 4 / 1 x 2 blocks (15 x 20 -> 8 x 5 blocks, 7 x 10 -> 7 x 5); every level starts on a
-    # 128-byte line
-    sizes = [60 * 80, 32 * 40, 8 * 5 * 8, 7 * 5 * 2]
+    # level 0 tiled (each image 4 x 8 tiles: 60x80 exactly); levels 1-3 interleaved in 2 x 4 / 2 x 4
+    # / 1 x 2 blocks (30 x 40 -> 15 x 10 blocks, 15 x 20 -> 8 x 5, 7 x 10 -> 7 x 5); every level
+    # starts on a 128-byte line
+    sizes = [60 * 80, 15 * 10 * 8, 8 * 5 * 8, 7 * 5 * 2]
     assert off == [0] + list(np.cumsum([76800 * s for s in sizes]))
     from eraft_amd.layout import formats
-    assert formats(60, 80, 4) == [10, 5, -5, -5]
-    assert formats(32, 32, 4) == [4, 2, -2, -2]       # MVSEC: 8 x 8 and 4 x 4 levels
-    assert formats(92, 160, 4) == [20, 10, -10, -10]  # 1280x720: 23 x 40 and 11 x 20 levels
-    # 3 rows: interleaved levels hold whole 64-row groups (5x5 -> 3 x 2 blocks of 8, 2x2 -> 2 x 1 of 2)
+    assert formats(60, 80, 4) == [10, -10, -5, -5]
+    assert formats(32, 32, 4) == [4, -4, -2, -2]      # MVSEC: 16 x 16, 8 x 8 and 4 x 4 levels
+    assert formats(92, 160, 4) == [20, -20, -10, -10]  # 1280x720: 46 x 80, 23 x 40 and 11 x 20 levels
+    # 3 rows: interleaved levels hold whole 64-row groups (10x10 -> 5 x 3 blocks of 8, 5x5 -> 3 x 2
+    # blocks of 8, 2x2 -> 2 x 1 of 2)
     _, _, off = _lib.layout(3, 20, 20, 4)
-    assert formats(20, 20, 4) == [3, 2, -2, -1]
-    assert off == [0, 1440, 2016, 2016 + 64 * 48, 2016 + 64 * 48 + 64 * 4]
+    assert formats(20, 20, 4) == [3, -3, -2, -1]
+    assert off == [0, 1440, 1440 + 64 * 120, 1440 + 64 * 120 + 64 * 48, 1440 + 64 * 120 + 64 * 48 + 64 * 4]
     # levels past 3 stay tiled, or compact where tiles would pad them by more than half
-    assert formats(64, 64, 6) == [8, 4, -4, -4, 0, 0]
-    assert formats(128, 256, 6) == [32, 16, -16, -16, 2, 1]
+    assert formats(64, 64, 6) == [8, -8, -4, -4, 0, 0]
+    assert formats(128, 256, 6) == [32, -32, -16, -16, 2, 1]
     th, tw = ctypes.c_int(), ctypes.c_int()
     assert ea.lib().ecorr_pyramid_tile(ctypes.byref(th), ctypes.byref(tw)) == 0
     assert (th.value, tw.value) == (4, 8)
@@ -140,10 +141,10 @@ def test_tile_untile_roundtrip():
 
 
 def test_interleaved_roundtrip():
-    """Levels 2-3: [64-row group][block][row][bh][bw] (include/ecorr.h), ragged rows and sides."""
+    """Levels 1-3: [64-row group][block][row][bh][bw] (include/ecorr.h), ragged rows and sides."""
     import torch
     from eraft_amd.layout import GROUP, tile, untile
-    for level, (bh, bw) in ((2, (2, 4)), (3, (1, 2))):
+    for level, (bh, bw) in ((1, (2, 4)), (2, (2, 4)), (3, (1, 2))):
         for rows, h, w in [(3, 15, 20), (130, 7, 10), (64, 1, 1), (65, 5, 9)]:
             lv = torch.arange(rows * h * w, dtype=torch.float32).reshape(rows, h, w)
             nbx, nby = -(-w // bw), -(-h // bh)
