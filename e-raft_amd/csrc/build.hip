@@ -662,6 +662,193 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
     split_epilogue<MUL>(P, acc, smem + wave * (4 * 32 * XS), wave * 64, exq, ext, fst, tc, b, q0, lane);
 }
 
+// ============================================================================================
+// fp32 GEMM for D = 256 (ecorr_build): build_split_kernel's structure -- 256 x 128 block tile, 4
+// waves of 64 queries x 128 targets, two blocks per CU, the register epilogue split_epilogue() --
+// on v_mfma_f32_32x32x2_f32 with the fp32 operands read straight from the fmaps (no operand pass):
+//   targets: chunk kc (16 k rows) goes global -> LDS by LDS-DMA as [k][128 targets in split_target
+//     order] (8 KB; a lane copies 4 adjacent pixels of one row, 16 bytes, so W % 4 == 0); the A
+//     fragment of group j, k-step s is one ds_read_b32 (lane (t, kh): target 32 j + t, k 2 s + kh);
+//   queries: the B fragment (lane (q, kh): query 32 i + q of the wave, k 2 s + kh) is one dword
+//     load per (i, s) from fmap1 [D][q_count] (a lane pair's 32 queries: two whole 128-byte rows).
+// Per element the k order is that of the fp32 build_kernel (chunks, k-steps, the MFMA's own k pair:
+// an exact k-ordered fmaf chain), so the pyramid is bitwise the same; the MFMA work per chunk (64
+// instructions per wave) is 5.3x the split kernel's, so operand traffic no longer binds.
+// ============================================================================================
+constexpr int FDT = 3;    // target chunks ahead (LDS buffers)
+constexpr int FDQ = 2;    // query chunks ahead (register sets)
+constexpr int FQL = 16;   // query dword loads per wave and chunk (2 groups x 8 k-steps)
+
+// VMEM instructions issued after t(j) when advance(j) waits for it (see split_vm_after)
+constexpr int f32_vm_after(int j, int nk) {
+    int n = 0;
+    bool seen = false;
+    for (int k = 0; k < FDT; ++k) {   // prologue: t(k) q(k)
+        if (seen) n += SCOPIES;
+        if (k == j) seen = true;
+        if (k < FDQ && k < nk && seen) n += FQL;
+    }
+    for (int c = 0; c <= j - 2; ++c) {   // chunk c: t(c + FDT), q(c + FDQ)
+        if (seen) n += SCOPIES;
+        if (c + FDT == j) seen = true;
+        if (c + FDQ < nk && seen) n += FQL;
+    }
+    return n;
+}
+// the waits as literals (hipcc does not fold the replay inside the unrolled loop):
+// advance(j) waits with 18 younger ops for j = 1, 2, 16 and 34 for j = 3 .. 15; the prologue with 36
+static_assert(f32_vm_after(0, 16) == 36 && f32_vm_after(1, 16) == 18 && f32_vm_after(2, 16) == 18 &&
+                  f32_vm_after(3, 16) == 34 && f32_vm_after(15, 16) == 34 && f32_vm_after(16, 16) == 18,
+              "fp32 loop wait counts");
+
+template <bool MUL>
+__global__ __launch_bounds__(256, 2) void build_f32_kernel(BuildParams P) {
+    constexpr int NK = 16;
+    __shared__ __attribute__((aligned(16))) char smem[SLDS + (SQ + 256) * 4];
+    int* exq = reinterpret_cast<int*>(smem + SLDS);
+    int* ext = exq + SQ;
+    float* fst = reinterpret_cast<float*>(ext + 128);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int b, qt, nt;
+    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    b = __builtin_amdgcn_readfirstlane(b);
+    qt = __builtin_amdgcn_readfirstlane(qt);
+    nt = __builtin_amdgcn_readfirstlane(nt);
+    const NTile tc = ntile_of(P, nt);
+    const int q0 = qt * SQ;
+    const int H = P.H, W = P.W;
+    const int64_t Q = (int64_t)H * W;
+    // no operand scaling: zero exponents make split_epilogue's scale 1 / sqrt(D) alone
+    exq[tid] = 0;
+    if (tid < 128) {
+        ext[tid] = 0;
+        fst[tid] = 1.0f;
+    }
+
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(P.f1 + (int64_t)b * P.D * P.q_count), 0, (int)((int64_t)P.D * P.q_count * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(P.f2 + (int64_t)b * P.D * Q), 0, (int)((int64_t)P.D * Q * 4), 0x00020000);
+    // DMA piece c = wave + 4 s of a chunk: k rows 2c, 2c + 1; lane l copies targets 4 (l & 31) .. +3
+    // of row 2c + (l >> 5) (4 adjacent pixels of one image row in split_target order)
+    // per-lane byte offsets fixed for the whole loop (the row-dependent part rides in the scalar
+    // soffset; a per-load select on the lane offset makes hipcc branch around every load)
+    int tvo;   // the lane's 4 pixels in k row (lane >> 5), or out of range outside the image
+    {
+        int y, x;
+        split_target(4 * (lane & 31), tc.band, y, x);
+        y += tc.ty0;
+        x += tc.tx0;
+        tvo = (y < H && x < W) ? (int)(((lane >> 5) * Q + (int64_t)y * W + x) * 4) : SOOB;
+    }
+    auto issue = [&](int kc) {
+        char* dst = smem + (kc % FDT) * SCHUNK;
+#pragma unroll
+        for (int s = 0; s < SCOPIES; ++s) {
+            const int c = wave + 4 * s;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + c * 1024), 16,
+                                                     tvo, kc < NK ? (int)((16 * kc + 2 * c) * Q * 4) : SOOB, 0, 0);
+        }
+    };
+
+    floatx16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
+
+    // query fragments: lane (q, kh) of group i, k-step s = fmap1[16 kc + 2 s + kh][q0 + 64 wave + 32 i + q]
+    struct QF { float v[2][8]; };
+    const int kh = lane >> 5;
+    int qvo[2];   // the lane's query in k row kh, or out of range past the slab
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int qq = q0 + 64 * wave + 32 * i + (lane & 31);
+        qvo[i] = qq < P.q_count ? (int)(((int64_t)kh * P.q_count + qq) * 4) : SOOB;
+    }
+    auto load_q = [&](int kc, QF& q) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                q.v[i][s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    rq, qvo[i], (int)((int64_t)(16 * kc + 2 * s) * P.q_count * 4), 0));
+    };
+    // target fragments from LDS: group j, k-step s at (2 s + kh) * 512 + (32 j + t) * 4
+    struct TF { float v[4][8]; };
+    const int tfo = kh * 512 + (lane & 31) * 4;
+    auto read_t = [&](int kc, TF& f, int s0) {
+        const char* cb = smem + (kc % FDT) * SCHUNK + tfo;
+#pragma unroll
+        for (int s = s0; s < s0 + 4; ++s)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) f.v[j][s] = *reinterpret_cast<const float*>(cb + s * 1024 + j * 128);
+    };
+    auto mfma_half = [&](const TF& f, const QF& q, int s0) {
+#pragma unroll
+        for (int s = s0; s < s0 + 4; ++s)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.v[j][s], q.v[i][s], acc[i][j], 0, 0, 0);
+    };
+#define PHASE __builtin_amdgcn_sched_barrier(0)
+    auto advance = [&](int j) {
+        PHASE;
+        if (j == 1 || j == 2 || j == NK) wait_vm<18, true>();
+        else wait_vm<34, true>();
+        __builtin_amdgcn_s_barrier();
+        PHASE;
+        issue(j + FDT - 1);
+        PHASE;
+    };
+    TF f[2];
+    QF qs[FDQ];
+#pragma unroll
+    for (int k = 0; k < FDT; ++k) {
+        issue(k);
+        PHASE;
+        if (k < FDQ) load_q(k, qs[k]);
+        PHASE;
+    }
+    wait_vm<36, true>();   // t(0) landed
+    __builtin_amdgcn_s_barrier();
+    PHASE;
+    read_t(0, f[0], 0);
+    read_t(0, f[0], 4);
+    PHASE;
+#pragma unroll
+    for (int kc = 0; kc < NK; ++kc) {
+        mfma_half(f[kc & 1], qs[kc % FDQ], 0);
+        PHASE;
+        advance(kc + 1);
+        read_t(kc + 1, f[(kc + 1) & 1], 0);
+        PHASE;
+        mfma_half(f[kc & 1], qs[kc % FDQ], 4);
+        PHASE;
+        read_t(kc + 1, f[(kc + 1) & 1], 4);
+        if (kc + FDQ < NK) load_q(kc + FDQ, qs[kc % FDQ]);
+        PHASE;
+    }
+#undef PHASE
+    wait_vm<0, true>();
+    __builtin_amdgcn_s_barrier();   // every wave is done with the chunk buffers (epilogue scratch)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
+    split_epilogue<MUL>(P, acc, smem + wave * (4 * 32 * XS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+}
+
 // Split-mode operand pass: per pixel, ex = 15 - E with max_d |x| = f 2^E, f in [0.5, 1) (so the
 // pixel's largest scaled value lies in [2^14, 2^15); 0 for all-zero or non-finite maxima, so NaN
 // inputs propagate through the GEMM as in the reference), and the f16 split of all D values:
@@ -1283,17 +1470,26 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
             else hipLaunchKernelGGL((build_split_kernel<false, 0>), grid, dim3(256), 0, stream, P);
         }
     } else {
-        const int64_t ntiles = (int64_t)B * P.n_mt * P.n_nt;
-        if (ntiles <= 0 || ntiles > 0x7fffffff) return ECORR_EINVAL;
-        const bool vec = (P.W % 4 == 0) && (P.q_count % 4 == 0) && ((uintptr_t)P.f1 % 16 == 0) &&
-                         ((uintptr_t)P.f2 % 16 == 0);
-        // LDS-DMA staging whenever both operands' byte offsets fit the 31-bit buffer range
-        const bool glds = vec && (int64_t)P.D * P.H * P.W * 4 < 0x7fff0000LL &&
-                          (int64_t)P.D * P.q_count * 4 < 0x7fff0000LL;
-        const dim3 grid((unsigned)ntiles), block(NT);
-        if (glds) hipLaunchKernelGGL((build_kernel<true, true>), grid, block, 0, stream, P);
-        else if (vec) hipLaunchKernelGGL((build_kernel<true, false>), grid, block, 0, stream, P);
-        else hipLaunchKernelGGL((build_kernel<false, false>), grid, block, 0, stream, P);
+        // D = 256 with 4-aligned rows and 31-bit operand offsets: the 256 x 128 fp32 kernel
+        if (P.D == 256 && P.W % 4 == 0 && (uintptr_t)P.f2 % 16 == 0 && (int64_t)P.D * P.H * P.W * 4 < 0x7fff0000LL &&
+            (int64_t)P.D * P.q_count * 4 < 0x7fff0000LL) {
+            const int64_t nt2 = (int64_t)B * P.n_qt * P.n_nt;
+            if (nt2 <= 0 || nt2 > 0x7fffffff) return ECORR_EINVAL;
+            if (P.scale_is_mul) hipLaunchKernelGGL((build_f32_kernel<true>), dim3((unsigned)nt2), dim3(256), 0, stream, P);
+            else hipLaunchKernelGGL((build_f32_kernel<false>), dim3((unsigned)nt2), dim3(256), 0, stream, P);
+        } else {   // any D: the 128 x 128 fp32 kernel
+            const int64_t ntiles = (int64_t)B * P.n_mt * P.n_nt;
+            if (ntiles <= 0 || ntiles > 0x7fffffff) return ECORR_EINVAL;
+            const bool vec = (P.W % 4 == 0) && (P.q_count % 4 == 0) && ((uintptr_t)P.f1 % 16 == 0) &&
+                             ((uintptr_t)P.f2 % 16 == 0);
+            // LDS-DMA staging whenever both operands' byte offsets fit the 31-bit buffer range
+            const bool glds = vec && (int64_t)P.D * P.H * P.W * 4 < 0x7fff0000LL &&
+                              (int64_t)P.D * P.q_count * 4 < 0x7fff0000LL;
+            const dim3 grid((unsigned)ntiles), block(NT);
+            if (glds) hipLaunchKernelGGL((build_kernel<true, true>), grid, block, 0, stream, P);
+            else if (vec) hipLaunchKernelGGL((build_kernel<true, false>), grid, block, 0, stream, P);
+            else hipLaunchKernelGGL((build_kernel<false, false>), grid, block, 0, stream, P);
+        }
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ECORR_EHIP - (int)e;
