@@ -332,28 +332,40 @@ def pmc_traffic(kernel_prefix):
     return None, f"no {kernel_prefix} record in profiles/latest_pmc.json"
 
 
-def measure_fp32_build(f1, f2, reps=5):
+def measure_fp32_build(f1, f2, reps=5, per=3):
     """The fp32-MFMA build (ecorr_build: v_mfma_f32_32x32x2_f32, an exact fmaf chain per element)
-    on the same inputs, outside the headline timed region: median of reps, HIP events."""
-    import eraft_amd
+    on the same inputs, outside the headline timed region: `per` back-to-back launches into one
+    preallocated pyramid between two HIP events on the launch stream (host gaps amortized), median
+    of reps after a warm-up."""
     from eraft_amd import _lib
     B, D, H, W = f1.shape
     _, _, off = _lib.layout(B * H * W, H, W, 4)
     stream = torch.cuda.current_stream(f1.device)
+    pyr = torch.empty(off[-1], dtype=torch.float32, device=f1.device)
+    st = _lib.stream_of(f2)
+
+    def launch():
+        _lib.check(_lib.lib().ecorr_build(f1.data_ptr(), f2.data_ptr(), B, D, H, W, H * W, 4, pyr.data_ptr(), st),
+                   "fp32 build")
+    launch()
+    torch.cuda.synchronize()
     ts = []
-    for _ in range(reps + 1):
+    for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        _lib.build_pyramid(f1, f2, B, D, H, W, H * W, 4, off, "fp32 build", mode="fp32")
+        for _ in range(per):
+            launch()
         e1.record(stream)
         torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1))
-    ms = sorted(ts[1:])[len(ts[1:]) // 2]
+        ts.append(e0.elapsed_time(e1) / per)
+    del pyr
+    ms = sorted(ts)[len(ts) // 2]
     flops = 2.0 * B * (H * W) ** 2 * D
     tf = flops / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4), "ms_per_launch": round(ms, 4),
-            "mode": "fp32", "covers": "build_kernel (v_mfma_f32_32x32x2_f32, one launch)",
+            "mode": "fp32", "covers": "build_f32_kernel (D = 256: v_mfma_f32_32x32x2_f32, fp32 operands straight "
+                                      "from the fmaps, one launch)",
             "note": "north_star's fp32-MFMA design; the headline uses the split build (more accurate vs fp64, "
                     "tests/test_build_modes_gpu.py)"}
 
