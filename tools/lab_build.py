@@ -269,6 +269,10 @@ for _dt in (3, 5, 6):
 # timing only: every block reads the same query / target panels (all L2 hits, same traffic to the CUs)
 PATCHES["sameq"] = [("build.hip", "P.pk1 + ((int64_t)b * P.n_mt + qp) * pstride", "P.pk1")]
 PATCHES["samet"] = [("build.hip", "P.pk2 + ((int64_t)b * P.n_nt + nt) * pstride", "P.pk2")]
+# epilogue pacing: s_sleep after each level-0 line's four stores (timing A/B; bitwise the same)
+for _sl in (2, 6, 16):
+    PATCHES[f"pace{_sl}"] = [("build.hip", "ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_L01);\n",
+                              f"ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_L01);\n        __builtin_amdgcn_s_sleep({_sl});\n")]
 COMBOS = {"loopstamps_epioob": ["loopstamps", "epioob"], "stamps_loopprio": ["stamps", "loopprio"], "stamps_stagger2": ["stamps", "stagger2"], "loopstamps_noepi": ["loopstamps", "noepi"], "loopstamps_noqdma": ["loopstamps", "noqdma"], "stamps_noqdma": ["noqdma", "stamps"], "stamps_prio": ["stamps", "prio"], "stamps_epioob": ["stamps", "epioob"], "stamps_epinost": ["stamps", "epinost"]}
 COMBOS.update({"loopstamps_qwait": ["loopstamps", "qwait"]})
 COMBOS.update({"stamps_epi_noscale": ["stamps", "epi_noscale"], "stamps_epi_nolds": ["stamps", "epi_nolds"]})
