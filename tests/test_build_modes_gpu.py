@@ -26,6 +26,8 @@ CASES = [  # (B, D, H, W, operand scale, seed)
     (1, 256, 60, 80, 1.0, 2),
     (2, 256, 32, 32, 1e-3, 3),
     (2, 256, 32, 32, 3e4, 4),
+    (2, 256, 45, 68, 1.0, 7),      # fp32 mode: build_f32_kernel with ragged query/target tiles
+    (1, 256, 19, 30, 1.0, 8),      # fp32 mode: W % 4 != 0 falls back to the generic kernel
     (1, 100, 17, 22, 1.0, 5),      # ragged: non-vector loads, D % 16 != 0
     (3, 64, 9, 13, 0.25, 6),
 ]
