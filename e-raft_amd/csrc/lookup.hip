@@ -54,12 +54,13 @@ __global__ __launch_bounds__(4 * QB) void lookup_staged(LookupParams P) {
 // columns (+ the two x end points for the window check) in registers, so the only LDS is the
 // windows and their origins (31.7 KB at r = 4: 5 blocks per CU).  Round-1 A/B: the 4-thread
 // kernel with per-output k decoding 61 vs 48.5 us; chains shared through LDS 2.8% slower.
-template <int R, int QB>
+// PAIR (every level width even): windows staged as 8-byte column pairs (lookup_stage.h).
+template <int R, int QB, bool PAIR>
 __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
     constexpr int NTQ = 3 * QB, K = 2 * R + 1, AP = K / 3;
     static_assert(K % 3 == 0 && QB == kWave, "one wave per part, whole columns per part");
-    using WB = WindowBuf<R, QB>;
-    constexpr int S = WB::S, SP = WB::SP, KK = WB::KK;
+    using WB = WindowBuf<R, QB, PAIR>;
+    constexpr int S = WB::S, SW = WB::SW, SP = WB::SP, KK = WB::KK;
     __shared__ WB st;
     const int tid = threadIdx.x, g = tid % QB;
     const int part = __builtin_amdgcn_readfirstlane(tid / QB);   // wave-uniform
@@ -85,14 +86,14 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
         coord_chain<R>(cx, K - 1, wm1, xl, dummy);
     }
     int org[3];
-    window_origin<S>(valid, x0, xl, fy[0], fy[K - 1], org);
+    window_origin<S, PAIR>(valid, x0, xl, fy[0], fy[K - 1], org);
     if (part == 0) {
         st.org[g][0] = org[0];
         st.org[g][1] = org[1];
         st.org[g][2] = org[2];
     }
     __syncthreads();
-    stage_windows<R, QB, NTQ>(st, P, lv, b, q0, tid);
+    stage_windows<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid);
 
     const int md = org[2] & 0xff;
     if (md == 2) return;   // past the range (no barrier follows)
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
     if (md == 0) {
         int yo[K];
 #pragma unroll
-        for (int bb = 0; bb < K; ++bb) yo[bb] = ((int)fy[bb] - org[1]) * S;
+        for (int bb = 0; bb < K; ++bb) yo[bb] = ((int)fy[bb] - org[1]) * SW;
         const float* wq = st.win + g * SP;
 #pragma unroll
         for (int ai = 0; ai < AP; ++ai) {
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
 #pragma unroll
             for (int bb = 0; bb < K; ++bb) {
                 const float* c = wc + yo[bb];
-                const float v = blend(c[0], c[1], c[S], c[S + 1], wx[ai], wy[bb]);
+                const float v = blend(c[0], c[1], c[SW], c[SW + 1], wx[ai], wy[bb]);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
                                                       sbase + (a * K + bb) * P.q_count * 4, 2);
             }
@@ -199,8 +200,15 @@ int launch_lookup(const LookupParams& P, int B, hipStream_t stream) {
     const dim3 grid((unsigned)((P.q_count + 63) / 64), (unsigned)P.levels, (unsigned)B);
     const bool cols = (P.radius == 4 || P.radius == 1) && (int64_t)P.C * P.q_count * 4 < 0x7fffffff;
     if (cols) {
-        if (P.radius == 4) hipLaunchKernelGGL((lookup_cols_reg<4, 64>), grid, dim3(192), 0, stream, P);
-        else hipLaunchKernelGGL((lookup_cols_reg<1, 64>), grid, dim3(192), 0, stream, P);
+        bool pair = true;   // column-pair staging: every level width even, 8-byte aligned levels
+        for (int lv = 0; lv < P.levels; ++lv) pair &= P.lw[lv] % 2 == 0 && (uintptr_t)P.lvl[lv] % 8 == 0;
+        if (P.radius == 4) {
+            if (pair) hipLaunchKernelGGL((lookup_cols_reg<4, 64, true>), grid, dim3(192), 0, stream, P);
+            else hipLaunchKernelGGL((lookup_cols_reg<4, 64, false>), grid, dim3(192), 0, stream, P);
+        } else {
+            if (pair) hipLaunchKernelGGL((lookup_cols_reg<1, 64, true>), grid, dim3(192), 0, stream, P);
+            else hipLaunchKernelGGL((lookup_cols_reg<1, 64, false>), grid, dim3(192), 0, stream, P);
+        }
         return hip_status();
     }
     switch (P.radius) {

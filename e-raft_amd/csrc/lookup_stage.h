@@ -17,16 +17,20 @@
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
 
+typedef unsigned uint2v __attribute__((ext_vector_type(2)));
+
 namespace ecorr {
 
-// The staged windows of QB queries and their origins (all phase 1 needs).
-template <int R, int QB>
+// The staged windows of QB queries and their origins (all phase 1 needs).  PAIR: the window is
+// staged as 8-byte column pairs from an even origin (every level width even), so a staged row
+// holds S + 1 columns.
+template <int R, int QB, bool PAIR = false>
 struct WindowBuf {
     static constexpr int K = 2 * R + 1;   // samples per axis
     static constexpr int KK = K * K;
-    static constexpr int S = 2 * R + 3;   // staged window side
-    static constexpr int SS = S * S;
-    static constexpr int SP = SS | 1;     // odd per-query stride: conflict-free lanes = queries
+    static constexpr int S = 2 * R + 3;   // staged window side (rows)
+    static constexpr int SW = PAIR ? S + 1 : S;   // staged row length
+    static constexpr int SP = (S * SW) | 1;       // odd per-query stride: conflict-free lanes = queries
     float win[QB * SP];
     // per query: window origin x, y and (mode | needed cols << 8 | needed rows << 16), where mode
     // 0 = staged, 1 = direct gather (coordinates that do not fit the window), 2 = past the range.
@@ -51,7 +55,8 @@ __device__ __forceinline__ void coord_chain(float cs, int o, float m1, float& f,
 }
 
 // Phase 0b for one query from its first / last x and y floors: origin and mode word (WindowBuf::org).
-template <int S>
+// PAIR: the origin column is rounded down to even and the needed columns counted from there.
+template <int S, bool PAIR = false>
 __device__ __forceinline__ void window_origin(bool valid, float x0, float xl, float y0, float yl, int org[3]) {
     int md = 2, X0 = 0, Y0 = 0, NX = 0, NY = 0;
     if (valid) {
@@ -67,15 +72,19 @@ __device__ __forceinline__ void window_origin(bool valid, float x0, float xl, fl
         // corners span [x0, floor(ix_last) + 1]: monotone round trip, so the last sample bounds it
         NX = ok ? (int)dx + 2 : 0;
         NY = ok ? (int)dy + 2 : 0;
+        if (PAIR) {
+            NX += X0 & 1;   // X0 may be negative: & ~1 rounds toward -inf
+            X0 &= ~1;
+        }
     }
     org[0] = X0;
     org[1] = Y0;
     org[2] = md | (NX << 8) | (NY << 16);
 }
 
-template <int R, int QB, int NTQ>
-__device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const LookupParams& P, int lv, int b, int q0,
-                                              int tid);
+template <int R, int QB, int NTQ, bool PAIR = false>
+__device__ __forceinline__ void stage_windows(WindowBuf<R, QB, PAIR>& st, const LookupParams& P, int lv, int b,
+                                              int q0, int tid);
 
 // Phases 0 and 1 for level lv of queries [q0, q0 + QB) of batch item b; ends with a barrier.
 template <int R, int QB, int NTQ>
@@ -115,11 +124,12 @@ __device__ __forceinline__ void stage_level(WindowStage<R, QB>& st, const Lookup
 }
 
 // Phase 1 for level lv of queries [q0, q0 + QB) of batch item b, from st.org; ends with a barrier.
-template <int R, int QB, int NTQ>
-__device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const LookupParams& P, int lv, int b, int q0,
-                                              int tid) {
-    using WS = WindowBuf<R, QB>;
-    constexpr int S = WS::S, SP = WS::SP;
+template <int R, int QB, int NTQ, bool PAIR>
+__device__ __forceinline__ void stage_windows(WindowBuf<R, QB, PAIR>& st, const LookupParams& P, int lv, int b,
+                                              int q0, int tid) {
+    using WS = WindowBuf<R, QB, PAIR>;
+    constexpr int S = WS::S, SW = WS::SW, SP = WS::SP;
+    constexpr int V = PAIR ? 2 : 1;   // window columns per work item (PAIR: one 8-byte load)
     const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
     const int64_t hw = P.lsz[lv];  // floats per query image
     const int64_t R0 = (int64_t)b * P.q_count + q0;   // first query row of the group
@@ -128,11 +138,14 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const Lookup
     const float* __restrict__ lvbase = P.lvl[lv] + (ntx < 0 ? g0 * kGroup * hw : R0 * hw);
 
     // ---- phase 1: stage windows, zeros outside the image (grid_sample padding_mode='zeros').
-    // Work item = (query, window column); each item walks the S rows.  Loads are raw buffer loads
+    // Work item = (query, window column or, PAIR, even column pair); each item walks the S rows.
+    // A pair never straddles the image edge (even origin, even width) and its two floats are
+    // adjacent in every layout (tile rows of 8, block rows of 4 or 2, image rows).  Loads are raw buffer loads
     // over this group's slab of the level: an element outside the image gets an out-of-range
     // offset and the hardware range check returns 0 -- zero padding with no branch and no select,
     // so all NCOL*S loads of a thread issue back to back.
-    constexpr int ITEMS = QB * S;
+    constexpr int NPX = SW / V;   // work items per query
+    constexpr int ITEMS = QB * NPX;
     constexpr int NCOL = (ITEMS + NTQ - 1) / NTQ;
     const int nq = min(QB, P.q_count - q0);
     const int64_t span = ntx < 0 ? (((R0 + nq - 1) >> 6) - g0 + 1) * kGroup * hw : nq * hw;
@@ -146,14 +159,14 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const Lookup
     const int step_in = 4 << sx;
     const int step_wrap = tiled ? 128 * ntx - 96 : ilv ? 4 * (-ntx * kGroup * (1 << (sy + sx)) - ymask * (1 << sx)) : 4 * w;
     constexpr int OOB = 0x7ffffff0;   // beyond any slab: reads as 0
-    float vals[NCOL][S];
+    float vals[NCOL][S][V];
     int dst[NCOL];
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
         const int it = tid + c * NTQ;
         const bool live = it < ITEMS;
-        const int gq = live ? it / S : 0;
-        const int rx = it - gq * S;
+        const int gq = live ? it / NPX : 0;
+        const int rx = (it - gq * NPX) * V;
         const int x = st.org[gq][0] + rx, y0 = st.org[gq][1], info = st.org[gq][2];
         const int ny = (info >> 16) & 0xff;
         // only the needed corner rectangle touches memory; the slack row/column reads 0 for free
@@ -179,7 +192,13 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const Lookup
 #pragma unroll
         for (int ry = 0; ry < S; ++ry) {
             const bool need = (unsigned)(ry - rlo) < (unsigned)(rhi - rlo);
-            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));
+            if constexpr (PAIR) {
+                const uint2v u = __builtin_amdgcn_raw_buffer_load_b64(rsrc, need ? off : OOB, 0, 0);
+                vals[c][ry][0] = __uint_as_float(u.x);
+                vals[c][ry][1] = __uint_as_float(u.y);
+            } else {
+            vals[c][ry][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));
+            }
             off += ym == ymask ? step_wrap : step_in;
             ym = (ym + 1) & ymask;
         }
@@ -188,7 +207,9 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB>& st, const Lookup
     for (int c = 0; c < NCOL; ++c)
         if (dst[c] >= 0)
 #pragma unroll
-            for (int ry = 0; ry < S; ++ry) st.win[dst[c] + ry * S] = vals[c][ry];
+            for (int ry = 0; ry < S; ++ry)
+#pragma unroll
+                for (int v = 0; v < V; ++v) st.win[dst[c] + ry * SW + v] = vals[c][ry][v];
     __syncthreads();
 }
 
@@ -211,6 +232,7 @@ __device__ __forceinline__ float sample_level(const WindowStage<R, QB>& st, cons
                                               int q0, int g, int k, int md) {
     using WS = WindowStage<R, QB>;
     constexpr int K = WS::K, S = WS::S, SP = WS::SP;
+    static_assert(WS::SW == S, "sample_level reads unpaired windows");
     const int a = k / K, bb = k - a * K;
     const float xa = st.fx[g][a], yb = st.fy[g][bb];
     const float wa = st.wx[g][a], nb = st.wy[g][bb];

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B of the radius-4 lookup between the tree's libecorr.so and AB_ALT_LIB lab builds
-(name=path,...) in ONE process, on one pyramid built by the tree library (DSEC B=16 60x80).
+(name=path,...) in ONE process, on one pyramid built by the tree library (DSEC B=16 60x80;
+coordinates AB_COORDS=smooth (default), int (zero flow) or rough (i.i.d. 12-px flow)).
 Checks first that every library's lookup is bitwise identical to the tree's (AB_NOCHECK=1 skips:
 ablation builds), then times 12 lookups per round in rotated order.
   AB_ALT_LIB=v=tools/v_lab/e-raft_amd/libecorr.so python tools/ab_lookup.py
@@ -44,13 +45,21 @@ with torch.no_grad():
     blk = eraft_amd.CorrBlock(f1, f2)
     base = eraft_amd.coords_grid(B, H, W, device="cuda")
     init = torch.nn.functional.avg_pool2d(torch.randn((B, 2, H, W), generator=g, device="cuda") * 9.0, 5, 1, 2)
-    coords = [(base + init + 0.5 * torch.randn((B, 2, H, W), generator=g, device="cuda")).contiguous()
-              for _ in range(12)]
+    mode = os.environ.get("AB_COORDS", "smooth")   # smooth | int (zero flow) | rough (i.i.d. flow)
+    if mode == "int":
+        coords = [base.clone() for _ in range(12)]
+    elif mode == "rough":
+        coords = [(base + 12.0 * torch.randn((B, 2, H, W), generator=g, device="cuda")).contiguous()
+                  for _ in range(12)]
+    else:
+        coords = [(base + init + 0.5 * torch.randn((B, 2, H, W), generator=g, device="cuda")).contiguous()
+                  for _ in range(12)]
     if not os.environ.get("AB_NOCHECK"):
-        ref = blk(coords[0])
+        checks = [coords[0], coords[0] + 0.3]   # + a non-integer shift (the int mode's floors flip)
+        refs = [blk(c) for c in checks]
         for name, L in LIBS.items():
             _lib._lib = L
-            same = torch.equal(blk(coords[0]), ref)
+            same = all(torch.equal(blk(c), r) for c, r in zip(checks, refs))
             print(f"bitwise {name}: {'same' if same else 'DIFFERENT'}", flush=True)
             if not same:
                 raise SystemExit(f"{name}: lookup differs")
@@ -71,6 +80,6 @@ with torch.no_grad():
     res = {}
     for name, ts in times.items():
         med = statistics.median(ts)
-        print(f"lookup B={B} {name:10s} median {med:.1f} us  min {min(ts):.1f}", flush=True)
+        print(f"lookup B={B} {mode} {name:10s} median {med:.1f} us  min {min(ts):.1f}", flush=True)
         res[name] = round(med, 1)
     print(json.dumps({"ab_lookup_us": res}))
