@@ -38,8 +38,8 @@ struct WindowBuf {
 };
 
 // ... plus the per-query coordinate chains in LDS (kernels whose threads share them).
-template <int R, int QB>
-struct WindowStage : WindowBuf<R, QB> {
+template <int R, int QB, bool PAIR = false>
+struct WindowStage : WindowBuf<R, QB, PAIR> {
     static constexpr int K = 2 * R + 1;
     float fx[QB][K], wx[QB][K], fy[QB][K], wy[QB][K];
 };
@@ -87,10 +87,10 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB, PAIR>& st, const 
                                               int q0, int tid);
 
 // Phases 0 and 1 for level lv of queries [q0, q0 + QB) of batch item b; ends with a barrier.
-template <int R, int QB, int NTQ>
-__device__ __forceinline__ void stage_level(WindowStage<R, QB>& st, const LookupParams& P, int lv, int b, int q0,
-                                            int tid) {
-    using WS = WindowStage<R, QB>;
+template <int R, int QB, int NTQ, bool PAIR = false>
+__device__ __forceinline__ void stage_level(WindowStage<R, QB, PAIR>& st, const LookupParams& P, int lv, int b,
+                                            int q0, int tid) {
+    using WS = WindowStage<R, QB, PAIR>;
     constexpr int K = WS::K, S = WS::S;
     constexpr int TPQ = NTQ / QB;   // threads per query
     const int g = tid % QB, part = tid / QB;
@@ -118,9 +118,9 @@ __device__ __forceinline__ void stage_level(WindowStage<R, QB>& st, const Lookup
     __syncthreads();
 
     // ---- phase 0b: window origin and fast/slow decision per query
-    if (part == 0) window_origin<S>(valid, st.fx[g][0], st.fx[g][K - 1], st.fy[g][0], st.fy[g][K - 1], st.org[g]);
+    if (part == 0) window_origin<S, PAIR>(valid, st.fx[g][0], st.fx[g][K - 1], st.fy[g][0], st.fy[g][K - 1], st.org[g]);
     __syncthreads();
-    stage_windows<R, QB, NTQ>(st, P, lv, b, q0, tid);
+    stage_windows<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid);
 }
 
 // Phase 1 for level lv of queries [q0, q0 + QB) of batch item b, from st.org; ends with a barrier.
@@ -227,12 +227,11 @@ __device__ __forceinline__ float sample_direct(const LookupParams& P, int lv, in
 }
 
 // Phase 2: sample k = a(2r+1) + b of query g (staged mode md = 0 or direct mode md = 1).
-template <int R, int QB>
-__device__ __forceinline__ float sample_level(const WindowStage<R, QB>& st, const LookupParams& P, int lv, int b,
-                                              int q0, int g, int k, int md) {
-    using WS = WindowStage<R, QB>;
-    constexpr int K = WS::K, S = WS::S, SP = WS::SP;
-    static_assert(WS::SW == S, "sample_level reads unpaired windows");
+template <int R, int QB, bool PAIR = false>
+__device__ __forceinline__ float sample_level(const WindowStage<R, QB, PAIR>& st, const LookupParams& P, int lv,
+                                              int b, int q0, int g, int k, int md) {
+    using WS = WindowStage<R, QB, PAIR>;
+    constexpr int K = WS::K, S = WS::SW, SP = WS::SP;   // S: the staged row length
     const int a = k / K, bb = k - a * K;
     const float xa = st.fx[g][a], yb = st.fy[g][bb];
     const float wa = st.wx[g][a], nb = st.wy[g][bb];

@@ -40,11 +40,12 @@ constexpr int KC = 16;     // channels per weight chunk
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-template <int R>
+// PAIR (every level width even): windows staged as 8-byte column pairs (lookup_stage.h).
+template <int R, bool PAIR>
 __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, const float* __restrict__ wt /* [O][C] */,
                                                              const float* __restrict__ bias, int O,
                                                              float* __restrict__ out) {
-    using WS = WindowStage<R, QBM>;
+    using WS = WindowStage<R, QBM, PAIR>;
     constexpr int KK = WS::KK;
     constexpr int CPAD = ((4 * KK + KC - 1) / KC) * KC;   // levels <= 4; rows padded to whole chunks
     __shared__ struct {
@@ -64,10 +65,10 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
 
     // ---- lookup: the block's corr tile, level by level, into T (rows >= C zero)
     for (int lv = 0; lv < P.levels; ++lv) {
-        stage_level<R, QBM, NTM>(u.st, P, lv, b, q0, tid);
+        stage_level<R, QBM, NTM, PAIR>(u.st, P, lv, b, q0, tid);
         const int md = u.st.org[g][2] & 0xff;
         if (md == 0) {   // staged window: origin hoisted, no mode test per sample
-            constexpr int K = WS::K, S = WS::S;
+            constexpr int K = WS::K, S = WS::SW;   // S: the staged row length
             const int o0 = u.st.org[g][0], o1 = u.st.org[g][1];
             const float* wq = u.st.win + g * WS::SP;
             // rows of each 16-row block: wave w, half h takes w + 8h and w + 4 + 8h
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
             for (int k0 = 0; k0 < KK; k0 += 2 * NTM / QBM)
                 for (int e = 0; e < 2; ++e) {
                     const int k = k0 + wave + 4 * e + 8 * half;
-                    if (k < KK) T[lv * KK + k][g] = md == 2 ? 0.0f : sample_level<R, QBM>(u.st, P, lv, b, q0, g, k, md);
+                    if (k < KK) T[lv * KK + k][g] = md == 2 ? 0.0f : sample_level<R, QBM, PAIR>(u.st, P, lv, b, q0, g, k, md);
                 }
         }
         __syncthreads();   // the stage is rebuilt by the next level / reused by the weight chunks
@@ -165,7 +166,10 @@ int launch_lookup_conv(const LookupParams& P, int B, const float* wt, const floa
     if (P.levels > 4) return ECORR_ELEVELS;
     if (O <= 0 || O % OW != 0) return ECORR_EINVAL;
     const dim3 grid((unsigned)((P.q_count + QBM - 1) / QBM), (unsigned)B), block(NTM);
-    hipLaunchKernelGGL(lookup_conv_kernel<4>, grid, block, 0, stream, P, wt, bias, O, out);
+    bool pair = true;   // column-pair staging: every level width even, 8-byte aligned levels
+    for (int lv = 0; lv < P.levels; ++lv) pair &= P.lw[lv] % 2 == 0 && (uintptr_t)P.lvl[lv] % 8 == 0;
+    if (pair) hipLaunchKernelGGL((lookup_conv_kernel<4, true>), grid, block, 0, stream, P, wt, bias, O, out);
+    else hipLaunchKernelGGL((lookup_conv_kernel<4, false>), grid, block, 0, stream, P, wt, bias, O, out);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
 }

@@ -251,6 +251,7 @@ PATCHES["loopstamps16"] = [
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
 PATCHES["nopair"] = [("lookup.hip", "        bool pair = true;", "        bool pair = false;")]
+PATCHES["nopairm"] = [("motion.hip", "    bool pair = true;", "    bool pair = false;")]
 # round-2 store ablations on the current epilogue (timing only): level-2/3 pixel stores issued out
 # of range / as non-temporal stores; level-0/1 line stores out of range
 _L23 = ["__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, 0);",
