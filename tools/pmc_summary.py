@@ -8,7 +8,7 @@ of its dominant kernel from profiles/latest_pmc.json, a copy of the newest summa
 HBM traffic per dispatch, corrected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
 coalesced read, so read bytes = 2 * FETCH_SIZE * 1024 for kernels whose loads are 16-byte
-vectors (the build).  The lookup's dword buffer loads are an uncalibrated width: its read bytes
+vectors (the build).  The lookup's 8-byte buffer loads are an uncalibrated width: its read bytes
 are reported uncorrected (1 * FETCH_SIZE) and flagged.  Infinity-Cache hits count as fabric
 traffic (the counters sit at the L2's memory side).
 """
