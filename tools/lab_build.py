@@ -252,6 +252,18 @@ PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
 PATCHES["nopair"] = [("lookup.hip", "        bool pair = true;", "        bool pair = false;")]
 PATCHES["nopairm"] = [("motion.hip", "    bool pair = true;", "    bool pair = false;")]
+# fused lookup + convc1 ablations (timing only, AB_NOCHECK=1): no GEMM phase / no lookup phase
+PATCHES["mo_nogemm"] = [("motion.hip", "    for (int oc = 0; oc < O; oc += OB) {", "    for (int oc = 0; oc < 0; oc += OB) {")]
+PATCHES["mo_nolookup"] = [("motion.hip", "    for (int lv = 0; lv < P.levels; ++lv) {\n        stage_level",
+                           "    for (int lv = 0; lv < 0; ++lv) {\n        stage_level")]
+# every lane reads the same 32 bytes of W (weight traffic ~0, same instructions)
+PATCHES["mo_samew"] = [("motion.hip", "        const int r0 = (ob + col) * C, r1 = (ob + 32 + col) * C;",
+                        "        const int r0 = 0 * (ob + col) * C, r1 = 0 * (ob + 32 + col) * C;")]
+PATCHES["mo_nolookup_samew"] = PATCHES["mo_nolookup"] + PATCHES["mo_samew"]
+# ... and without the MFMAs (fragments kept alive): is the matrix pipe what bounds the GEMM phase?
+PATCHES["mo_nolookup_nomfma"] = PATCHES["mo_nolookup"] + [("motion.hip", """                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[j >> 2][j & 3], bq[j], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[2 + (j >> 2)][j & 3], bq[j], acc1, 0, 0, 0);""",
+    """                asm volatile("" :: "v"(wc[j >> 2][j & 3]), "v"(wc[2 + (j >> 2)][j & 3]), "v"(bq[j]));""")]
 # round-2 store ablations on the current epilogue (timing only): level-2/3 pixel stores issued out
 # of range / as non-temporal stores; level-0/1 line stores out of range
 _L23 = ["__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, 0);",
