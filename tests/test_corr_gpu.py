@@ -213,3 +213,30 @@ def test_geometry_vs_oracle(ea, geom):
     for i in range(1, L):
         assert oracle.same_bits(levels[i], ref_levels[i]), f"level {i}"
     assert oracle.same_bits(out, oracle.lookup(levels, coords, 4))
+
+
+# Column-pair window staging (every level width even, lookup_stage.h) vs single columns (some level
+# width odd): floor flips of integer coordinates, half-pixel shifts, windows hanging over every
+# image edge, and NaN / inf / huge coordinates (the direct path), bit-exact vs the oracle.
+@pytest.mark.parametrize("shape", [(2, 32, 24, 32, 4), (1, 32, 20, 36, 4), (1, 16, 60, 80, 4)],
+                         ids=["pairs_24x32", "single_20x36", "pairs_60x80"])
+def test_lookup_adversarial_coords(ea, shape):
+    B, D, H, W, L = shape
+    f1, f2 = prng.normal(51, (B, D, H, W)), prng.normal(52, (B, D, H, W))
+    ys, xs = np.meshgrid(np.arange(H, dtype=np.float32), np.arange(W, dtype=np.float32), indexing="ij")
+    grid = np.broadcast_to(np.stack([xs, ys])[None], (B, 2, H, W)).astype(np.float32)
+    edge = grid.copy()
+    edge[:, 0, :, :4] = np.float32(-4.5) - edge[:, 0, :, :4]              # left of the image
+    edge[:, 0, :, -4:] += np.float32(3.7)                                  # right of it
+    edge[:, 1, :2] = np.float32(-0.999)                                    # just above
+    edge[:, 1, -2:] = np.float32(H - 1) + np.float32(2.25)                 # below
+    odd = prng.coords_with_flow(53, B, H, W, 6.0).astype(np.float32)   # 6-px random flow
+    odd[0, :, 0, :6] = np.array([[np.nan, np.inf, -np.inf, 1e9, -7.0e5, 3.0e7]] * 2, dtype=np.float32)
+    sets = {"int": grid, "half": grid + np.float32(0.5), "edge": edge, "odd": odd}
+    with torch.no_grad():
+        blk = ea.CorrBlock(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L)
+        levels = [lv[:, 0].cpu().numpy() for lv in blk.corr_pyramid]
+        for name, c in sets.items():
+            c = np.ascontiguousarray(c, dtype=np.float32)
+            out = blk(torch.from_numpy(c).to(DEV)).cpu().numpy()
+            assert oracle.same_bits(out, oracle.lookup(levels, c, 4)), name
