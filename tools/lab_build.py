@@ -264,6 +264,10 @@ PATCHES["mo_nolookup_samew"] = PATCHES["mo_nolookup"] + PATCHES["mo_samew"]
 PATCHES["mo_nolookup_nomfma"] = PATCHES["mo_nolookup"] + [("motion.hip", """                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[j >> 2][j & 3], bq[j], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[2 + (j >> 2)][j & 3], bq[j], acc1, 0, 0, 0);""",
     """                asm volatile("" :: "v"(wc[j >> 2][j & 3]), "v"(wc[2 + (j >> 2)][j & 3]), "v"(bq[j]));""")]
+# ... and without the output stores (the epilogue's bias loads kept)
+PATCHES["mo_nolookup_nomfma_nost"] = PATCHES["mo_nolookup_nomfma"] + [("motion.hip", "                        out[((int64_t)b * O + o) * P.q_count + q] = v < 0.0f ? 0.0f : v;   // NaN stays NaN",
+    "                        if (v == 1234.5f) out[((int64_t)b * O + o) * P.q_count + q] = v;")]
+PATCHES["mo_nolookup_nost"] = PATCHES["mo_nolookup"] + PATCHES["mo_nolookup_nomfma_nost"][-1:]
 # round-2 store ablations on the current epilogue (timing only): level-2/3 pixel stores issued out
 # of range / as non-temporal stores; level-0/1 line stores out of range
 _L23 = ["__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, 0);",
