@@ -240,3 +240,18 @@ def test_lookup_adversarial_coords(ea, shape):
             c = np.ascontiguousarray(c, dtype=np.float32)
             out = blk(torch.from_numpy(c).to(DEV)).cpu().numpy()
             assert oracle.same_bits(out, oracle.lookup(levels, c, 4)), name
+
+
+# The reference's own outputs through the column-pair staging: the golden cases' leading levels whose
+# widths are all even (t16x24: 24, 12, 6; b2_8x12: 12, 6) looked up alone give the reference's
+# leading channels, bit-exact, for every golden coordinate set (integer, near-integer, special).
+@pytest.mark.parametrize("name,L", [("corr_t16x24", 3), ("corr_b2_8x12", 2)])
+def test_golden_pair_staging(ea, name, L):
+    z = _load(os.path.join(GOLDEN, name + ".npz"))
+    r, W = int(z["r"]), int(z["W"])
+    assert all((W >> i) % 2 == 0 for i in range(L))   # the column-pair path
+    K = 2 * r + 1
+    levels = [z[f"level{i}"] for i in range(L)]
+    for s in [k[len("coords_"):] for k in z if k.startswith("coords_")]:
+        got = _lookup_on(ea, levels, z[f"coords_{s}"], r)
+        assert oracle.same_bits(got, z[f"out_{s}"][:, :L * K * K]), s
