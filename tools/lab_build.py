@@ -251,6 +251,12 @@ PATCHES["loopstamps16"] = [
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
 PATCHES["nopair"] = [("lookup.hip", "        bool pair = true;", "        bool pair = false;")]
+# lookup wave priority: raised while the window loads issue (phase 1) / while the outputs store
+PATCHES["lk_prio1"] = [("lookup_stage.h", "    float vals[NCOL][S][V];\n    int dst[NCOL];\n",
+                        "    float vals[NCOL][S][V];\n    int dst[NCOL];\n    __builtin_amdgcn_s_setprio(2);\n"),
+                       ("lookup_stage.h", "                for (int v = 0; v < V; ++v) st.win[dst[c] + ry * SW + v] = vals[c][ry][v];\n    __syncthreads();\n}",
+                        "                for (int v = 0; v < V; ++v) st.win[dst[c] + ry * SW + v] = vals[c][ry][v];\n    __builtin_amdgcn_s_setprio(0);\n    __syncthreads();\n}")]
+PATCHES["lk_prio2"] = [("lookup.hip", "    if (md == 0) {\n        int yo[K];", "    __builtin_amdgcn_s_setprio(2);\n    if (md == 0) {\n        int yo[K];")]
 PATCHES["nopairm"] = [("motion.hip", "    bool pair = true;", "    bool pair = false;")]
 # fused lookup + convc1 ablations (timing only, AB_NOCHECK=1): no GEMM phase / no lookup phase
 PATCHES["mo_nogemm"] = [("motion.hip", "    for (int oc = 0; oc < O; oc += OB) {", "    for (int oc = 0; oc < 0; oc += OB) {")]
