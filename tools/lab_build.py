@@ -251,6 +251,10 @@ PATCHES["loopstamps16"] = [
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
 PATCHES["nopair"] = [("lookup.hip", "        bool pair = true;", "        bool pair = false;")]
+# timing only: no window loads for one level (what does each level's staging cost?)
+for _lv in range(4):
+    PATCHES[f"lk_skip{_lv}"] = [("lookup_stage.h", "            const bool need = (unsigned)(ry - rlo) < (unsigned)(rhi - rlo);",
+                                 f"            const bool need = lv != {_lv} && (unsigned)(ry - rlo) < (unsigned)(rhi - rlo);")]
 # lookup wave priority: raised while the window loads issue (phase 1) / while the outputs store
 PATCHES["lk_prio1"] = [("lookup_stage.h", "    float vals[NCOL][S][V];\n    int dst[NCOL];\n",
                         "    float vals[NCOL][S][V];\n    int dst[NCOL];\n    __builtin_amdgcn_s_setprio(2);\n"),
