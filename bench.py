@@ -313,12 +313,19 @@ def measure_voxel(device, n=1_000_000, C=15, H=480, W=640, reps=5):
                     "GPU uses float atomics: not reproducible); normalization within 1e-6"}
 
 
-def pmc_traffic(kernel_prefix):
+def shape_key(B, D, H, W, q):
+    """The launch shape a PMC record belongs to: batch, feature width, query pixels per pair (the
+    slab, row-shard mode), target map."""
+    return f"B{B}_D{D}_q{q}_{H}x{W}"
+
+
+def pmc_traffic(kernel_prefix, key, path=None):
     """HBM bytes per dispatch of the dominant kernel from the committed PMC summary
-    (profiles/latest_pmc.json, tools/pmc_summary.py), used only when its kernel-source digest is
-    this tree's (a summary of other kernels is refused, not reported)."""
+    (profiles/latest_pmc.json, tools/pmc_summary.py), keyed by launch shape: used only when the
+    summary's kernel-source digest is this tree's AND it holds a record of this very shape (a
+    summary of other kernels or of another config is refused, not reported)."""
     import eraft_amd
-    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
+    path = path or os.path.join(ROOT, "profiles", "latest_pmc.json")
     try:
         js = json.load(open(path))
     except (OSError, ValueError):
@@ -326,10 +333,75 @@ def pmc_traffic(kernel_prefix):
     here = eraft_amd._lib.source_digest()
     if js.get("source_digest") != here:
         return None, f"refused: profiles/latest_pmc.json measured sources {js.get('source_digest')}, tree is {here}"
-    for name, rec in js.get("kernels", {}).items():
+    shapes = js.get("shapes", {})
+    if key not in shapes:
+        return None, f"refused: shape {key} not profiled (profiled: {sorted(shapes)})"
+    for name, rec in shapes[key].get("kernels", {}).items():
         if name.startswith(kernel_prefix) and "hbm_bytes" in rec:
-            return rec["hbm_bytes"], f"{js.get('source', path)}: {name} ({rec.get('read_correction')}), sources {here}"
-    return None, f"no {kernel_prefix} record in profiles/latest_pmc.json"
+            return rec["hbm_bytes"], (f"{js.get('source', path)}: {name} at {key} ({rec.get('read_correction')}), "
+                                      f"sources {here}")
+    return None, f"no {kernel_prefix} record at {key} in profiles/latest_pmc.json"
+
+
+def measure_lookup_fields(blk, B, H, W, iters, look_bytes, device, reps=3):
+    """SURVEY 8(d)'s coordinate fields beside the bench's smooth warm-start one: coords_grid + i.i.d.
+    N(0, 3 px) flow (the primary synthetic input) and the sigma = 40 px stress field (mostly out of
+    bounds); `iters` distinct fields each, 12 lookups between two HIP events on the launch stream,
+    median of reps after a warm-up, outside the headline timed region."""
+    import eraft_amd
+    g = torch.Generator(device=device).manual_seed(77)
+    base = eraft_amd.coords_grid(B, H, W, device=device)
+    stream = torch.cuda.current_stream(device)
+    res = {}
+    for name, sigma in (("lookup_iid", 3.0), ("lookup_stress", 40.0)):
+        cs = [(base + sigma * torch.randn((B, 2, H, W), generator=g, device=device)).contiguous()
+              for _ in range(iters)]
+        ts = []
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for c in cs:
+                blk(c)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / iters)
+        ms = sorted(ts[1:])[len(ts[1:]) // 2]
+        gbs = look_bytes / (ms * 1e-3) / 1e9
+        res[name] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(ms, 4),
+                     "coords": f"coords_grid + i.i.d. N(0, {sigma:g} px) flow, {iters} fields"}
+    return res
+
+
+def measure_fp32_step(make_block, coords, B, iters, ideal_s, reps=5):
+    """North star's literal fp32-MFMA configuration as a whole step (ecorr_build, build_f32_kernel,
+    + the 12 lookups), outside the headline timed region: reps steps between two HIP events on the
+    launch stream after a warm-up step, the build mode restored afterwards."""
+    import eraft_amd
+    prev = eraft_amd._lib.build_mode()
+    eraft_amd._lib.set_build_mode("fp32")
+    try:
+        stream = torch.cuda.current_stream()
+
+        def step():
+            blk = make_block()
+            for c in coords:
+                blk(c)
+        step()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            step()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+    finally:
+        eraft_amd._lib.set_build_mode(prev)
+    return {"pairs_per_s": round(B / (ms * 1e-3), 2), "ms_per_step": round(ms, 4), "steps": reps,
+            "corrblock_frac": round(ideal_s / (ms * 1e-3), 4), "mode": "fp32",
+            "covers": f"ecorr_build (build_f32_kernel, v_mfma_f32_32x32x2_f32) + {iters} lookups per step",
+            "ideal": "fp32-MFMA roof for the build + the lookups at 8 TB/s"}
 
 
 def measure_fp32_build(f1, f2, reps=5, per=3):
@@ -509,10 +581,20 @@ def main():
         ("build_kernel" if dom == "build" else "lookup_cols_reg")
     if dom == "build" and mode == "split":
         roof["window_frac"] = kernels["build"]["window"]["frac"]
-    traffic, src = pmc_traffic(roof["kernel"])
+    key = shape_key(B, D, H, W, q_local)
+    traffic, src = pmc_traffic(roof["kernel"], key)
+    roof["shape_key"] = key
     roof["traffic"] = traffic
     roof["traffic_source"] = src
     ideal_s = max(t_mfma, t_hbm) + iters * look_bytes / (PEAK_HBM_GBS * 1e9)
+    if a.mode == "batch":
+        with torch.no_grad():
+            kernels.update(measure_lookup_fields(make_block(), B, H, W, iters, look_bytes, device))
+    if mode == "split" and a.mode == "batch" and world == 1 and not a.no_next:
+        t32 = flops / (PEAK_FP32_MFMA_TFLOPS * 1e12)
+        with torch.no_grad():
+            kernels["fp32_step"] = measure_fp32_step(make_block, coords, B, iters,
+                                                     max(t32, t_hbm) + iters * look_bytes / (PEAK_HBM_GBS * 1e9))
     pairs = (world * B if a.mode == "batch" else B) * a.steps
     if a.mode == "batch":
         if (H, W) == (60, 80):
@@ -526,11 +608,27 @@ def main():
         cfg = {"workload": wl,
                "global_batch": world * B, "fmap": [D, H, W], "levels": 4, "radius": 4,
                "parallelism": f"dp{world} batch-sharded, no collective"}
+        if distributed:
+            # every rank's own pairs: the sum of its fmap1, gathered after the timed region
+            chk = torch.tensor([float(f1.double().sum())], dtype=torch.float64,
+                               device="cpu" if single else device)
+            allc = [torch.zeros_like(chk) for _ in range(world)]
+            dist.all_gather(allc, chk)
+            cfg["rank_input_checksums"] = [float(c.item()) for c in allc]
+            cfg["rank_seeds"] = [1234 + r for r in range(world)]
     else:
         cfg = {"workload": f"1280x720 CorrBlock build + {iters} lookups, batch {B}, query rows sharded "
                            f"over {world} GPUs (BASELINE configs[4])",
                "global_batch": B, "fmap": [D, H, W], "levels": 4, "radius": 4,
                "parallelism": f"query-row shard x{world}, RCCL all-gather of fmap2 + output slabs"}
+        # after the timed region, on every rank: one sharded lookup (the production exchange: RCCL
+        # into the persistent chunks + ecorr_rows_assemble) against the unsharded block, bitwise
+        with torch.no_grad():
+            same = torch.equal(make_block()(coords[0]), eraft_amd.CorrBlock(f1, f2)(coords[0]))
+        ok = torch.tensor([1.0 if same else 0.0], dtype=torch.float64, device="cpu" if single else device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        cfg["check_vs_unsharded"] = "bit-exact" if ok.item() == 1.0 else "DIFFERS"
+        cfg["row_partition"] = row_partition(H, world)[1]
     res = {
         "metric": METRIC, "value": round(pairs / elapsed, 2), "unit": "pairs/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
@@ -550,6 +648,8 @@ def main():
         res["cpu_baseline"] = cpu_baseline(f1, f2, coords, iters)
     if rank == 0:
         print(json.dumps(res), flush=True)
+    if cfg.get("check_vs_unsharded") == "DIFFERS":
+        raise SystemExit("row-sharded lookup differs from the unsharded CorrBlock")
     if distributed:
         dist.destroy_process_group()
 

@@ -246,6 +246,7 @@ __global__ __launch_bounds__(NTV) void norm_apply(float* __restrict__ g, int64_t
 // phase 3 scans each tile from its offset.  Integer arithmetic: exact in any order.
 constexpr int SCAN_PER = 16, SCAN_T = NTV * SCAN_PER;
 
+static_assert(NTV % 64 == 0 && NTV <= 1024, "block_exclusive_scan: whole 64-lane waves, sh[NTV / 64]");
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     uint32_t x = v;
@@ -256,9 +257,13 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
     }
     if (lane == 63) sh[wv] = x;
     __syncthreads();
-    uint32_t pre = 0;
-    for (int w = 0; w < wv; ++w) pre += sh[w];
-    total = sh[0] + sh[1] + sh[2] + sh[3];
+    uint32_t pre = 0, sum = 0;
+#pragma unroll
+    for (int w = 0; w < NTV / 64; ++w) {
+        if (w < wv) pre += sh[w];
+        sum += sh[w];
+    }
+    total = sum;
     __syncthreads();
     return pre + x - v;
 }

@@ -46,6 +46,12 @@ class RowExchange:
     recv = world chunks.  Usage: fill send_slab(...) in place, then gather(...).  gather_chunks
     (the collective alone) also runs on CPU tensors, which is how the gloo tests check the chunk
     layout; the reassembly is the HIP kernel and needs a HIP device.
+
+    The send / receive buffers are reused by every gather, which is safe because the collective
+    is synchronous and runs on the launch stream (NCCL/RCCL enqueue on the current stream): the
+    next fill of the send chunk is stream-ordered after the previous collective read it.  Do not
+    call gather_chunks with async_op or from a side stream, and do not hold a returned receive
+    buffer across the next gather.
     """
 
     def __init__(self, H, group=None):

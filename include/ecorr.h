@@ -88,7 +88,11 @@ int ecorr_build_split(const float* fmap1, const float* fmap2, int B, int D, int 
 /* ecorr_build_split as its two stream-ordered stages, for callers that overlap or time them:
  * _pack = the operand pass (per-pixel exponents + f16 hi/lo panels into the workspace; reads
  * fmap1/fmap2), _gemm = the correlation GEMM with the fused pyramid (reads only the workspace).
- * pack then gemm on one stream == ecorr_build_split, bit for bit. */
+ * pack then gemm on one stream == ecorr_build_split, bit for bit.  Contract: both stages take the
+ * SAME workspace and IDENTICAL geometry (B, D, H, W, q_count), gemm stream-ordered after pack.  The
+ * workspace carries no header (a check would need a host read of device memory, i.e. a sync), so a
+ * gemm on a workspace packed for other geometry, or never packed, yields garbage exponents and
+ * panels rather than an error. */
 int ecorr_build_split_pack(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int q_count,
                            void* workspace, void* stream);
 int ecorr_build_split_gemm(int B, int D, int H, int W, int q_count, int levels, float* pyramid,

@@ -62,6 +62,20 @@ def coords_with_flow(seed: int, B: int, H: int, W: int, sigma: float) -> np.ndar
     return np.ascontiguousarray(grid + normal(seed, (B, 2, H, W), sigma))
 
 
+def coords_smooth(seed: int, B: int, H: int, W: int, sigma: float = 9.0, jitter: float = 0.5) -> np.ndarray:
+    """coords_grid + a smooth warm-start flow (5 x 5 box mean of N(0, sigma^2), zero-padded, /25 as
+    avg_pool2d's count_include_pad) + N(0, jitter^2): the field shape of bench.py's coordinates."""
+    n = normal(seed, (B, 2, H + 4, W + 4), sigma).astype(np.float64)
+    n[:, :, :2] = 0.0
+    n[:, :, -2:] = 0.0
+    n[:, :, :, :2] = 0.0
+    n[:, :, :, -2:] = 0.0
+    c = np.cumsum(np.cumsum(np.pad(n, ((0, 0), (0, 0), (1, 0), (1, 0))), axis=2), axis=3)
+    box = (c[:, :, 5:, 5:] - c[:, :, :-5, 5:] - c[:, :, 5:, :-5] + c[:, :, :-5, :-5]) / 25.0
+    flow = box.astype(np.float32) + normal(seed + 1, (B, 2, H, W), jitter)
+    return np.ascontiguousarray(coords_with_flow(0, B, H, W, 0.0) + flow)
+
+
 def dsec_events(seed: int, n: int, H: int, W: int):
     """Synthetic DSEC events as the loader hands them to VoxelGrid.convert (loader_dsec.py:245-257):
     fp32 p in {0, 1}, t ascending from 0 (us), rectified x / y reaching slightly outside the image."""

@@ -186,3 +186,23 @@ def test_pmc_source_digest_matches_library_digest(ea):
     ns = {"__file__": path}
     exec(compile(src.split("root = sys.argv[1]")[0], path, "exec"), ns)
     assert ns["source_digest"]() == ea._lib.source_digest()
+
+
+def test_pmc_traffic_is_shape_keyed(tmp_path):
+    """bench.py reports roofline.traffic only from a PMC record of its own launch shape and its own
+    kernel sources; another config's record is refused (the C5 line carried C2's bytes)."""
+    import json
+    import bench
+    import eraft_amd
+    dig = eraft_amd._lib.source_digest()
+    rec = {"kernels": {"build_split_kernel<true, 16>": {"hbm_bytes": 2.29e9, "read_correction": "x2"}}}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"source": "t", "source_digest": dig, "shapes": {"B16_D256_q4800_60x80": rec}}))
+    got, src = bench.pmc_traffic("build_split_kernel", "B16_D256_q4800_60x80", str(p))
+    assert got == 2.29e9 and "B16_D256_q4800_60x80" in src
+    got, src = bench.pmc_traffic("build_split_kernel", "B4_D256_q14720_92x160", str(p))
+    assert got is None and src.startswith("refused: shape")
+    p.write_text(json.dumps({"source": "t", "source_digest": "0" * 16, "shapes": {"B16_D256_q4800_60x80": rec}}))
+    got, src = bench.pmc_traffic("build_split_kernel", "B16_D256_q4800_60x80", str(p))
+    assert got is None and src.startswith("refused")
+    assert bench.shape_key(4, 256, 92, 160, 92 * 160) == "B4_D256_q14720_92x160"

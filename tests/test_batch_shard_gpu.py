@@ -1,0 +1,49 @@
+"""World-size-2 run of the batch-sharded bench path (BASELINE configs[3]).
+
+bench.py launched by torch.distributed.run with 2 processes, both on cuda:0 (BENCH_SINGLE_DEVICE=1:
+gloo for the timing max-reduce, set in the launcher's environment before any GPU call): each rank
+builds and looks up its OWN batch of pairs (seed 1234 + rank), no data-path collective, and rank 0
+reports the whole job.  Checks: n_gpus, the global batch (2 x 16), distinct per-rank inputs, and
+value = pairs of all ranks / the max-reduced elapsed time.  One GPU shared by two ranks measures
+the path, not the scaling: the 1/2/4/8-GPU curve is the driver's 8-GPU run.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_batch_shard():
+    steps, B = 2, 16
+    env = dict(os.environ, BENCH_SINGLE_DEVICE="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", str(steps), "--warmup", "1",
+           "--batch", str(B), "--no-next", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]   # rank 0 alone prints
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == steps and res["scaling"] == "weak"
+    cfg = res["config"]
+    assert cfg["global_batch"] == 2 * B
+    assert cfg["rank_seeds"] == [1234, 1235]
+    c0, c1 = cfg["rank_input_checksums"]
+    assert c0 != c1, "both ranks built the same pairs"
+    elapsed = res["ms_per_step"] * steps / 1e3
+    assert res["value"] == pytest.approx(2 * B * steps / elapsed, rel=1e-3)
+    assert res["kernels"]["build"]["ms_per_launch"] > 0 and res["kernels"]["lookup"]["ms_per_launch"] > 0

@@ -131,38 +131,49 @@ def test_large_against_reference_samples(ea, name):
 
 
 # BASELINE configs at their per-GPU batch: configs[1] DSEC B=16 (the bench line), configs[2] MVSEC
-# 32 x 32 at B=64, configs[3]'s per-GPU slice (DSEC B=256 over 8 GPUs = B=32)
-BATCH_CONFIGS = [(16, 60, 80, 11), (64, 32, 32, 31), (32, 60, 80, 41)]
+# 32 x 32 at B=64, configs[3]'s per-GPU slice (DSEC B=256 over 8 GPUs = B=32), configs[4]'s whole
+# 1280 x 720 job (fmap 92 x 160 after the 736-row pad, B=4; the row-sharded ranks build slabs of it,
+# bitwise its rows: tests/test_rowshard_gpu.py)
+BATCH_CONFIGS = [(16, 60, 80, 11, 2), (64, 32, 32, 31, 2), (32, 60, 80, 41, 2), (4, 92, 160, 61, 16)]
 
 
-@pytest.mark.parametrize("cfg", BATCH_CONFIGS, ids=["c2_dsec_b16", "c3_mvsec_b64", "c4_slice_dsec_b32"])
+@pytest.mark.parametrize("cfg", BATCH_CONFIGS, ids=["c2_dsec_b16", "c3_mvsec_b64", "c4_slice_dsec_b32",
+                                                   "c5_92x160_b4"])
 def test_bench_config_full_size(ea, cfg):
-    """Pooling and the full lookup bit-exact vs the oracle at the config's full size, GEMM
-    normwise on sampled query rows (every batch item), repeat calls bitwise deterministic."""
-    B, H, W, seed = cfg
+    """Pooling and the full lookup bit-exact vs the oracle at the config's full size (D = 256, the
+    split build's <true, 16> K loop), GEMM normwise on sampled query rows of every batch item,
+    lookups on two coordinate fields (coords_grid + i.i.d. N(0, 3 px) flow, and the
+    bench's smooth warm-start field), repeat calls bitwise deterministic."""
+    B, H, W, seed, per_b = cfg
     D = 256
     f1 = torch.from_numpy(prng.normal(seed, (B, D, H, W))).to(DEV)
     f2 = torch.from_numpy(prng.normal(seed + 1, (B, D, H, W))).to(DEV)
-    coords_np = prng.coords_with_flow(seed + 2, B, H, W, 3.0)
-    coords = torch.from_numpy(coords_np).to(DEV)
+    fields = {"iid3": prng.coords_with_flow(seed + 2, B, H, W, 3.0),
+              "smooth": prng.coords_smooth(seed + 3, B, H, W)}
+    outs = {}
     with torch.no_grad():
         blk = ea.CorrBlock(f1, f2)
-        out = blk(coords)
-        out2 = blk(coords)
+        for name, c in fields.items():
+            ct = torch.from_numpy(c).to(DEV)
+            outs[name] = blk(ct)
+            assert torch.equal(outs[name], blk(ct)), name
         torch.cuda.synchronize()
-    assert torch.equal(out, out2)
     levels = [lv[:, 0].cpu().numpy() for lv in blk.corr_pyramid]
     ref_levels = oracle.pyramid_from_level0(levels[0], 4)
     for i in range(1, 4):
         assert oracle.same_bits(levels[i], ref_levels[i]), f"level {i}"
-    # sampled rows: 2 per batch item (first item's first query, then a stride through the map)
-    rows = [b * H * W + (b * 997) % (H * W) for b in range(B)] + [b * H * W + H * W - 1 - b for b in range(B)]
+    del ref_levels
+    # sampled rows: per_b per batch item (spread through the map, first and last query included)
+    Q = H * W
+    rows = [b * Q + p for b in range(B) for p in
+            sorted({0, Q - 1 - b} | {(b * 997 + k * 7919) % Q for k in range(per_b - 2)})]
     f1n, f2n = f1.cpu().numpy(), f2.cpu().numpy()
     for rw in rows:
-        b, p = divmod(int(rw), H * W)
+        b, p = divmod(int(rw), Q)
         ref = oracle.corr_level0(f1n[b:b + 1], f2n[b:b + 1], p, 1)[0]
-        assert oracle.normwise_err(levels[0][rw], ref) <= GEMM_TOL
-    assert oracle.same_bits(out.cpu().numpy(), oracle.lookup(levels, coords_np, 4))
+        assert oracle.normwise_err(levels[0][rw], ref) <= GEMM_TOL, f"row {rw}"
+    for name, c in fields.items():
+        assert oracle.same_bits(outs[name].cpu().numpy(), oracle.lookup(levels, c, 4)), name
 
 
 def test_errors_match_reference(ea):

@@ -18,4 +18,17 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GR
   echo "pmc pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/pmc$i.log; exit $rc; fi
 done
+# HBM traffic of the other BASELINE configs (bench.py's roofline.traffic is keyed by launch shape)
+for cfg in "c3:--batch 64 --height 32 --width 32" "c5:--mode rowshard"; do
+  name=${cfg%%:*}; cargs=${cfg#*:}
+  mkdir -p $OUT/$name
+  j=0
+  for grp in FETCH_SIZE WRITE_SIZE; do
+    j=$((j+1))
+    timeout -k 10 120 rocprofv3 --pmc $grp -d $OUT/$name/pmc$j -o run --output-format csv -- python3 bench.py $cargs --steps 3 --warmup 1 --no-cpu-baseline --no-next > $OUT/$name/pmc$j.log 2>&1
+    rc=$?
+    echo "$name pmc pass $j ($grp) rc=$rc"
+    if [ $rc -ne 0 ]; then tail -5 $OUT/$name/pmc$j.log; exit $rc; fi
+  done
+done
 find $OUT -name '*.csv' | head -50
