@@ -48,6 +48,9 @@ with torch.no_grad():
     mode = os.environ.get("AB_COORDS", "smooth")   # smooth | int (zero flow) | rough (i.i.d. flow)
     if mode == "int":
         coords = [base.clone() for _ in range(12)]
+    elif mode.startswith("iid"):   # iid<sigma>: SURVEY 8(d)'s i.i.d. N(0, sigma^2) flow (iid3, iid40)
+        coords = [(base + float(mode[3:]) * torch.randn((B, 2, H, W), generator=g, device="cuda")).contiguous()
+                  for _ in range(12)]
     elif mode == "rough":
         coords = [(base + 12.0 * torch.randn((B, 2, H, W), generator=g, device="cuda")).contiguous()
                   for _ in range(12)]

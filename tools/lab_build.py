@@ -247,6 +247,20 @@ PATCHES["loopstamps16"] = [
     __builtin_amdgcn_s_barrier();   // every wave is done with the ring"""),
     ("build.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + STAMP_EXPORT),
 ]
+# round-3 per-block stamps of the split build: [start, K loop done, epilogue done, prologue done
+# (first barrier: exponents in LDS, t(0) landed), HW_ID | XCC_ID] -> tools/stamps.py --prologue
+PATCHES["stamps4"] = [
+    ("build.hip", "constexpr int SQ = 256; ", STAMP_DECL + "constexpr int SQ = 256; "),
+    ("build.hip", "    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n    int b, qt, nt;\n    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);\n    const NTile tc = ntile_of(P, nt);\n    const int q0 = qt * SQ;\n    const int H = P.H, W = P.W;\n    const int64_t Q = (int64_t)H * W;\n\n    {   // per-pixel",
+     "    stamp(0);\n    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;\n    int b, qt, nt;\n    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);\n    const NTile tc = ntile_of(P, nt);\n    const int q0 = qt * SQ;\n    const int H = P.H, W = P.W;\n    const int64_t Q = (int64_t)H * W;\n\n    {   // per-pixel"),
+    ("build.hip", "        wait_vm_n<true>(split_vm_after(0, NK));   // t(0) landed\n        __builtin_amdgcn_s_barrier();\n",
+     "        wait_vm_n<true>(split_vm_after(0, NK));   // t(0) landed\n        __builtin_amdgcn_s_barrier();\n        stamp(3);\n"),
+    ("build.hip", "    __builtin_amdgcn_s_barrier();   // ... in every wave: the chunk buffers are the epilogue's scratch\n",
+     "    __builtin_amdgcn_s_barrier();   // ... in every wave: the chunk buffers are the epilogue's scratch\n    stamp(1);\n"),
+    ("build.hip", "    split_epilogue<MUL>(P, acc, smem + wave * (4 * 32 * XS), wave * 64, exq, ext, fst, tc, b, q0, lane);\n}\n\n// ====",
+     "    split_epilogue<MUL>(P, acc, smem + wave * (4 * 32 * XS), wave * 64, exq, ext, fst, tc, b, q0, lane);\n    __syncthreads();\n    stamp(2);\n}\n\n// ===="),
+    ("build.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + STAMP_EXPORT),
+]
 # the tree as it is (the baseline of an A/B against an edited tree)
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs

@@ -51,6 +51,22 @@ print(f"loop  us: median {np.median(loop):.2f} p10 {np.percentile(loop, 10):.2f}
 iss = us(t3 - t1)
 print(f"epilogue issue (all waves' stores issued) us: median {np.median(iss):.2f} p10 {np.percentile(iss, 10):.2f} p90 {np.percentile(iss, 90):.2f}")
 print(f"epi   us: median {np.median(epi):.2f} p10 {np.percentile(epi, 10):.2f} p90 {np.percentile(epi, 90):.2f}")
+if os.environ.get("STAMPS_PROLOGUE"):   # stamps4: slot 3 = prologue done (first barrier, t(0) landed)
+    pro = us(t3 - t0)
+    core = us(t1 - t3)
+    print(f"prologue us: median {np.median(pro):.2f} p10 {np.percentile(pro, 10):.2f} p90 {np.percentile(pro, 90):.2f}")
+    print(f"K loop (after prologue) us: median {np.median(core):.2f} p10 {np.percentile(core, 10):.2f} p90 {np.percentile(core, 90):.2f}")
+    # dispatch gap: on each CU slot, the time from one block's end to the next block's start
+    gaps = []
+    for idx in [v for v in [[i for i in range(n) if (int(xcc[i]), int(cu[i])) == k] for k in list({(int(xcc[i]), int(cu[i])) for i in range(0, n, 97)})[:32]]]:
+        ends = sorted(t2[idx])
+        starts = sorted(t0[idx])
+        for s0 in starts[2:]:
+            prev = [e for e in ends if e <= s0]
+            if prev:
+                gaps.append(us(s0 - prev[-1]))
+    if gaps:
+        print(f"block start after the previous block end on the CU (us): median {np.median(gaps):.2f} p90 {np.percentile(gaps, 90):.2f}")
 # per CU: slots, busy fraction, overlap of one block's epilogue with another's loop
 cus = collections.defaultdict(list)
 for i in range(n):
