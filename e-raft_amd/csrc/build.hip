@@ -447,19 +447,20 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
     const int H = P.H, W = P.W;
     const int64_t Q = (int64_t)H * W;
 
-    {   // per-pixel exponents (written before the first barrier; the K loop's first wait drains
-        // them with lgkmcnt(0))
-        exq[tid] = q0 + tid < P.q_count ? P.ex1[(int64_t)b * P.q_count + q0 + tid] : 0;
+    // per-pixel exponents: only the epilogue reads them, so they load behind the K loop's last
+    // static wait and reach LDS after it (in the prologue, their two dependent global loads with
+    // vmcnt(0) waits delayed every block's first DMA)
+    int eq = 0, et = 0;
+    auto load_exponents = [&]() {
+        eq = q0 + tid < P.q_count ? P.ex1[(int64_t)b * P.q_count + q0 + tid] : 0;
         if (tid < 128) {
             int y, x;
             split_target(tid, tc.band, y, x);
             y += tc.ty0;
             x += tc.tx0;
-            const int e = (y < H && x < W) ? -P.ex2[(int64_t)b * Q + (int64_t)y * W + x] : 0;
-            ext[tid] = e;
-            fst[tid] = exp2i(max(-63, min(e, 63)));
+            et = (y < H && x < W) ? P.ex2[(int64_t)b * Q + (int64_t)y * W + x] : 0;   // negated after the loop
         }
-    }
+    };
 
     // ---- operand panels of this tile: two query panels (adjacent tiles of pk1), one target panel
     const int dc = (P.D + 15) / 16, nk = NK ? NK : dc;
@@ -598,6 +599,7 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
             mfma_lohi(f[kc & 1], qs[kc % SDQ]);
             PHASE;
             advance_n(kc + 1);
+            if (kc == NK - 1) load_exponents();   // after the last static wait
             read_lo(kc + 1, f[(kc + 1) & 1]);
             PHASE;
             mfma_rest(f[kc & 1], qs[kc % SDQ]);
@@ -651,8 +653,14 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
     }
     }
 #undef PHASE
-    wait_vm<0, true>();             // the trailing zero chunks have landed and this wave's reads are done ...
-    __builtin_amdgcn_s_barrier();   // ... in every wave: the chunk buffers are the epilogue's scratch
+    if constexpr (NK == 0) load_exponents();
+    wait_vm<0, true>();             // the exponents and the trailing zero chunks have landed, this wave's reads are done ...
+    exq[tid] = eq;
+    if (tid < 128) {
+        ext[tid] = -et;
+        fst[tid] = exp2i(max(-63, min(-et, 63)));
+    }
+    __syncthreads();                // ... in every wave: the chunk buffers are the epilogue's scratch
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -660,6 +668,382 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
 
     // ---------------- epilogue (per wave, from registers) ----------------
     split_epilogue<MUL>(P, acc, smem + wave * (4 * 32 * XS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+}
+
+// ============================================================================================
+// Split GEMM on v_mfma_f32_16x16x32_f16 (D = 256, the E-RAFT feature width: the default build).
+// The same block tile, waves and operand split as build_split_kernel (256 queries x one 128-target
+// n-tile, wave w = queries 64 w .. + 63 x all 128 targets, two blocks per CU, lo*hi + hi*lo + hi*hi
+// per product), on the 16x16x32 MFMA shape: at the same cycles per FLOP the chip holds a higher
+// clock under this load on 16x16x32 than on 32x32x16 (MI355X_MICROARCH.md, DVFS give-back item 7;
+// round-2 lab: 1.81 vs 1.49 GHz in the K loop alone, profiles/r02_lab/NOTES.md).
+//
+// K is consumed in 32-deep chunk pairs (the panel layout of pack_body<., true>): per pair and 16x16
+// tile three MFMAs, hi*hi, lo*hi, hi*lo, each over the pair's 32 k -- every fragment is loaded once
+// and used twice.  The MFMAs take the fmap2 fragment as A (16 targets x 32 k) and the query
+// fragment as B (32 k x 16 queries), so lane l of tile (query group qg, target group tg) holds
+// query 16 qg + (l & 15) and targets 16 tg + 4 kb + i, kb = l >> 4, i = 0..3.  The fmap2 panel
+// stores the n-tile's targets in split16_target order, which makes a lane's 32 targets of a
+// query one 4 x 8 quadrant of the 8 x 16 tile (band: one 4 x 8 block of the 4 x 32 tile) -- one
+// level-0 tile line, in line order (value 4 tg + i) -- so levels 1 and 2 pool in-lane and the 8 x 8
+// pool of level 3 needs one value from lane l ^ 16.
+//
+// K loop (8 chunk pairs): the target panel of a pair (16 KB, shared by the 4 waves) goes global ->
+// LDS by LDS-DMA (4 pieces per wave) through 4 buffers, two pairs ahead; the wave-private query
+// fragments (8 x 16 B per lane and pair) global -> VGPR one pair ahead.  One barrier per pair, in
+// the middle of the pair's 8 target groups (after group 5): it publishes the next pair (whose first
+// A fragments are then read under the last two groups' MFMAs) and retires every wave's reads of the
+// pair before, whose buffer the DMA two pairs ahead then takes.  Every wait is a static vmcnt that
+// assumes the source's VMEM issue order (s16_vm_after), fenced by sched_barrier; the CPU test
+// tests/test_isa_waits.py replays the emitted order.
+// ============================================================================================
+constexpr int PANEL16 = 2 * PANEL;              // bytes of one (128-pixel tile, 32-deep chunk pair) panel
+constexpr int NCP = 8;                          // chunk pairs at D = 256
+constexpr int S16NB = 4;                        // LDS buffers (chunk pairs) of the target panel
+constexpr int S16COPIES = PANEL16 / 1024 / 4;   // LDS-DMA pieces per wave and pair (4)
+constexpr int S16QL = 8;                        // query fragment loads per wave and pair
+constexpr int S16LS = 144;                      // LDS bytes per level-0 line in the epilogue transpose
+static_assert(S16NB * PANEL16 <= SLDS && 4 * 2 * 64 * S16LS <= SLDS, "split16 LDS regions");
+
+// target (y, x) of position p of a split16 fmap2 panel, relative to the n-tile origin: p = 16 tg +
+// 4 kb + i lies in quadrant kb (regular: rows 4 (kb & 1) .., cols 8 (kb >> 1) ..; band: cols 8 kb ..)
+// at quadrant row tg >> 1, column 4 (tg & 1) + i
+__host__ __device__ __forceinline__ void split16_target(int p, bool band, int& y, int& x) {
+    const int tg = p >> 4, kb = (p >> 2) & 3, i = p & 3;
+    if (!band) {
+        y = 4 * (kb & 1) + (tg >> 1);
+        x = 8 * (kb >> 1) + 4 * (tg & 1) + i;
+    } else {
+        y = tg >> 1;
+        x = 8 * kb + 4 * (tg & 1) + i;
+    }
+}
+
+// VMEM instructions a wave issues after the last piece of t(j) until the wait for t(j) (j >= 1: in
+// mid(j - 1)).  Issue order: prologue t(0) .. t(S16NB - 2), q(0); pair c: q(c + 1) (c + 1 < NCP),
+// then at its mid barrier (c + 1 < NCP) the wait for t(c + 1) and t(c + S16NB - 1) (< NCP).
+constexpr int s16_vm_after(int j) {
+    int n = 0;
+    bool seen = false;
+    for (int k = 0; k < S16NB - 1; ++k) {
+        if (seen) n += S16COPIES;
+        if (k == j) seen = true;
+    }
+    if (j == 0) return n + S16QL;   // the prologue's wait: t(1) .. t(NB - 2), q(0)
+    n += seen ? S16QL : 0;          // q(0)
+    for (int c = 0; c + 1 < NCP; ++c) {
+        if (seen) n += S16QL;       // q(c + 1)
+        if (c + 1 == j) return n;   // mid(c)
+        const int k = c + S16NB - 1;
+        if (k < NCP) {
+            if (seen) n += S16COPIES;
+            if (k == j) seen = true;
+        }
+    }
+    return n;
+}
+static_assert(S16NB != 4 || S16COPIES != 4 || S16QL != 8 ||
+                  (s16_vm_after(0) == 16 && s16_vm_after(1) == 20 && s16_vm_after(2) == 28 &&
+                   s16_vm_after(3) == 20 && s16_vm_after(6) == 20 && s16_vm_after(7) == 16),
+              "split16 wait counts (hand-checked for 4 buffers, 4 pieces, 8 query loads)");
+
+// Epilogue of build_split16_kernel for one wave: its 64 queries (block-local qw .. qw + 63) x the
+// n-tile tc from its accumulators acc[qg][tg]; xw = the wave's two LDS transpose regions (2 x 64
+// lines x S16LS bytes).
+template <bool MUL>
+__device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (&acc)[4][8], char* const xw, int qw,
+                                                 const int* exq, const int* ext, const float* fst, const NTile& tc,
+                                                 int b, int q0, int lane) {
+    const int qn = lane & 15, kb = lane >> 4;
+    const int L = P.fused_levels;
+    const int64_t rows0 = (int64_t)b * P.q_count + q0;   // the block's first query image
+    const int nq = min(SQ, P.q_count - q0);
+    const int64_t g0 = rows0 >> 6;
+    auto rsrc_of = [&](int lv) {
+        if (lv >= 1)
+            return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + g0 * kGroup * P.lsz[lv], 0,
+                                                     (int)((((rows0 + nq - 1) >> 6) - g0 + 1) * kGroup * P.lsz[lv] * 4),
+                                                     0x00020000);
+        return __builtin_amdgcn_make_buffer_rsrc(P.lvl[lv] + rows0 * P.lsz[lv], 0, (int)(nq * P.lsz[lv] * 4), 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t r0 = rsrc_of(0);
+    const __amdgpu_buffer_rsrc_t r1 = rsrc_of(L > 1 ? 1 : 0);
+    const __amdgpu_buffer_rsrc_t r2 = rsrc_of(L > 2 ? 2 : 0);
+    const __amdgpu_buffer_rsrc_t r3 = rsrc_of(L > 3 ? 3 : 0);
+    // level-0 line (tile row, tile col) of quadrant k of the n-tile
+    auto line_tr = [&](int k) { return (tc.ty0 >> 2) + (tc.band ? 0 : (k & 1)); };
+    auto line_tc = [&](int k) { return (tc.tx0 >> 3) + (tc.band ? k : (k >> 1)); };
+    // Level-0 transpose: lane l writes its line (query qn, quadrant kb) as line l of the region;
+    // store instruction s then takes lines s + 8 j, j = 0..7 (queries s, s + 8 of every quadrant),
+    // lane l piece pc of line s + 8 jl, with (jl, pc) chosen so that each 16-lane group of the
+    // ds_read_b128 ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, +32) reads two lines 8 apart: all 64
+    // banks (line stride 144 B = 36 dwords, 8 lines = 32 banks).
+    int jl, pc;
+    {
+        const int l = lane & 31;
+        const bool g1 = (l >= 4 && l < 12) || (l >= 16 && l < 20) || l >= 28;
+        const bool second = g1 ? l >= 12 : l >= 16;
+        pc = g1 ? (second ? (l < 20 ? l - 16 : l - 24) : l - 4) : (second ? l - 20 : (l < 4 ? l : l - 8));
+        jl = 4 * (lane >> 5) + 2 * (g1 ? 1 : 0) + (second ? 1 : 0);
+    }
+    const int lq = jl & 1 ? 8 : 0, lk = jl >> 1;   // line s + 8 jl: query s + lq, quadrant lk
+    const int ltr = line_tr(lk), ltc = line_tc(lk);
+    const bool lok = ltr < P.lnty[0] && ltc < P.lntx[0];
+    const int loff = ((ltr * P.lntx[0] + ltc) * kTile) * 4 + 16 * pc;
+    // One interleaved-level piece: query qloc (block-local), level pixel (r, c), N floats in a row.
+    // Queries past the block and blocks outside the level are dropped.
+    auto store_px = [&](__amdgpu_buffer_rsrc_t rs, int lv, int qloc, int r, int c, auto val, bool on) {
+        constexpr int N = sizeof(val) / 4;
+        const int sy = ilv_sy(lv), sx = ilv_sx(lv);
+        const int by = r >> sy, bx = c >> sx;
+        const bool in = on && qloc < nq && by < P.lnty[lv] && bx < -P.lntx[lv];
+        const int64_t R = rows0 + qloc;
+        const int off = (int)((((R >> 6) - g0) * kGroup * P.lsz[lv] +
+                               ((int64_t)(by * -P.lntx[lv] + bx) * kGroup + (R & (kGroup - 1))) * (1 << (sy + sx)) +
+                               ((r & ((1 << sy) - 1)) << sx) + (c & ((1 << sx) - 1))) * 4);
+        if constexpr (N == 4)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, ST_L01);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, val), rs, in ? off : SOOB, 0, ST_L01);
+    };
+    // fast scale: every exponent of the wave's queries and of the panel's targets in [-63, 63]
+    bool fast_scale;
+    {
+        const int n = -(exq[qw + lane] + (MUL ? P.scale_shift : 0));
+        fast_scale = __all(ext[lane] >= -63 && ext[lane] <= 63 && ext[lane + 64] >= -63 && ext[lane + 64] <= 63 &&
+                           n >= -63 && n <= 63);
+    }
+#pragma unroll
+    for (int qg = 0; qg < 4; ++qg) {
+        const int ql = qw + 16 * qg;   // block-local first query of the group
+        const int nqe = -(exq[ql + qn] + (MUL ? P.scale_shift : 0));
+        // v[tg][i] = quadrant pixel (tg >> 1, 4 (tg & 1) + i) of query ql + qn, quadrant kb
+        float v[8][4];
+        if (fast_scale) {
+            const float sq = exp2i(nqe);
+#pragma unroll
+            for (int tg = 0; tg < 8; ++tg) {
+                const floatx4 s4 = *reinterpret_cast<const floatx4*>(fst + 16 * tg + 4 * kb);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float x = __fmul_rn(acc[qg][tg][i], __fmul_rn(sq, s4[i]));
+                    v[tg][i] = MUL ? x : __fdiv_rn(x, P.scale);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int tg = 0; tg < 8; ++tg) {
+                const int4 e4 = *reinterpret_cast<const int4*>(ext + 16 * tg + 4 * kb);
+                const int e[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float x = ldexpf(acc[qg][tg][i], nqe + e[i]);
+                    v[tg][i] = MUL ? x : __fdiv_rn(x, P.scale);
+                }
+            }
+        }
+        // level 0: the line through the region (a wave's LDS accesses are processed in order, so
+        // group qg + 2's writes cannot overtake group qg's reads of the same region)
+        char* const xr = xw + (qg & 1) * (64 * S16LS);
+#pragma unroll
+        for (int tg = 0; tg < 8; ++tg)
+            *reinterpret_cast<floatx4*>(xr + lane * S16LS + 16 * tg) = floatx4{v[tg][0], v[tg][1], v[tg][2], v[tg][3]};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const floatx4 pcv = *reinterpret_cast<const floatx4*>(xr + (s + 8 * jl) * S16LS + 16 * pc);
+            const int qloc = ql + s + lq;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, pcv), r0,
+                                                   lok && qloc < nq ? (int)(qloc * P.lsz[0] * 4) + loff : SOOB, 0,
+                                                   ST_L01);
+        }
+        if (L < 2) continue;
+        // level 1: the quadrant's 2 x 4 block, l1[r][c] from quadrant rows 2r, 2r + 1, cols 2c, 2c + 1
+        auto q0v = [&](int yy, int xx) { return v[2 * yy + (xx >> 2)][xx & 3]; };
+        float l1[2][4];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                l1[r][c] = pool4_v(q0v(2 * r, 2 * c), q0v(2 * r, 2 * c + 1), q0v(2 * r + 1, 2 * c), q0v(2 * r + 1, 2 * c + 1));
+        float l2[2];
+        if (L >= 3) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) l2[c] = pool4_v(l1[0][2 * c], l1[0][2 * c + 1], l1[1][2 * c], l1[1][2 * c + 1]);
+        }
+        // level-1 stores: one swap of 16-lane rows (kb odd rows <-> kb even rows) leaves lane kb with
+        // block-row kb & 1 of the blocks of quadrants kb & ~1 (x) and kb | 1 (y): per instruction,
+        // 16 queries x 32 B contiguous per block, two blocks
+        {
+            float x[4], y[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                x[c] = l1[0][c];
+                y[c] = l1[1][c];
+                const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[c]), __float_as_uint(y[c]), false, false);
+                x[c] = __uint_as_float(sw[0]);
+                y[c] = __uint_as_float(sw[1]);
+            }
+            const int ke = kb & ~1, ko = kb | 1;
+            // block (ty0 / 4 + ..., tx0 / 8 + ...) of quadrant k at level 1; the lane's block row kb & 1
+            store_px(r1, 1, ql + qn, 2 * (line_tr(ke)) + (kb & 1), 4 * line_tc(ke), floatx4{x[0], x[1], x[2], x[3]}, true);
+            store_px(r1, 1, ql + qn, 2 * (line_tr(ko)) + (kb & 1), 4 * line_tc(ko), floatx4{y[0], y[1], y[2], y[3]}, true);
+        }
+        if (L < 3) continue;
+        // level 2: the quadrant's 1 x 2 pixels, row ty0 / 4 + (kb & 1) (band: ty0 / 4), cols tx0 / 4 +
+        // 2 (kb >> 1) (band: + 2 kb): 4 lanes x 8 B = one query's 2 x 4 block (band: half of two)
+        store_px(r2, 2, ql + qn, line_tr(kb), 2 * line_tc(kb), floatx2{l2[0], l2[1]}, true);
+        if (L < 4 || tc.band) continue;
+        // level 3 (regular tiles): pixel kb >> 1 of the tile's 1 x 2 from the 2 x 2 level-2 pixels of
+        // lanes kb (row 0, kb even) and kb + 1 (row 1); lane kb = 0 stores both pixels
+        const float o0 = __shfl_xor(l2[0], 16), o1 = __shfl_xor(l2[1], 16);
+        const float p3 = pool4_v(l2[0], l2[1], o0, o1);
+        const float p3b = __shfl_xor(p3, 32);   // lane kb = 0 <- kb = 2
+        store_px(r3, 3, ql + qn, tc.ty0 >> 3, tc.tx0 >> 3, floatx2{p3, p3b}, kb == 0);
+    }
+}
+
+template <bool MUL>
+__global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
+    // ALL LDS in this one array (cdna_hip_programming.md trap 4(a), see build_split_kernel)
+    __shared__ __attribute__((aligned(16))) char smem[SLDS + (SQ + 256) * 4];
+    int* exq = reinterpret_cast<int*>(smem + SLDS);   // exponents of the 256 queries
+    int* ext = exq + SQ;                              // ... negated, of the 128 panel targets
+    float* fst = reinterpret_cast<float*>(ext + 128);  // 2^ext when |ext| <= 63
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int b, qt, nt;
+    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    const NTile tc = ntile_of(P, nt);
+    const int q0 = qt * SQ;
+    const int H = P.H, W = P.W;
+    const int64_t Q = (int64_t)H * W;
+
+    // per-pixel exponents: loaded behind the K loop's last static wait (only the epilogue reads them)
+    int eq = 0, et = 0;
+    auto load_exponents = [&]() {
+        eq = q0 + tid < P.q_count ? P.ex1[(int64_t)b * P.q_count + q0 + tid] : 0;
+        if (tid < 128) {
+            int y, x;
+            split16_target(tid, tc.band, y, x);
+            y += tc.ty0;
+            x += tc.tx0;
+            et = (y < H && x < W) ? P.ex2[(int64_t)b * Q + (int64_t)y * W + x] : 0;   // negated after the loop
+        }
+    };
+
+    const int64_t pstride = (int64_t)NCP * PANEL16;   // bytes of one 128-pixel tile's panels
+    const int qp = 2 * qt;
+    const int nqp = min(2, P.n_mt - qp);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(P.pk1 + ((int64_t)b * P.n_mt + qp) * pstride), 0, (int)(nqp * pstride), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(P.pk2 + ((int64_t)b * P.n_nt + nt) * pstride), 0, (int)pstride, 0x00020000);
+    // target panel of pair cp: DMA piece c = wave + 4 s of its 16 KB (lane-linear); the pair and
+    // piece offsets ride in the scalar soffset, so one VGPR addresses every piece of the loop
+    const int tvo = wave * 1024 + lane * 16;
+    auto issue = [&](int cp) {
+        char* dst = smem + (cp % S16NB) * PANEL16;
+#pragma unroll
+        for (int s = 0; s < S16COPIES; ++s)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + (wave + 4 * s) * 1024),
+                                                     16, tvo, cp * PANEL16 + s * 4096, 0, 0);
+    };
+
+    floatx4 acc[4][8];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[g][t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(acc[g][t]));
+
+    // query fragments of the wave's 4 groups (panel wave / 2, 16-query groups 4 (wave & 1) + g), one pair
+    struct QF { halfx8 h[4], l[4]; };
+    const int qgo = (wave >> 1) * (int)pstride + (wave & 1) * (4 * 2048) + lane * 16;
+    auto load_q = [&](int cp, QF& q) {   // (pair, group) offset in the scalar soffset
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            q.h[g] = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(rq, qgo, cp * PANEL16 + g * 2048, 0));
+            q.l[g] = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(rq, qgo + 1024, cp * PANEL16 + g * 2048, 0));
+        }
+    };
+    // target fragments of group tg from LDS (lane-linear ds_read_b128, conflict-free)
+    struct AF { halfx8 h, l; };
+    auto read_a = [&](int cp, int tg, AF& a) {
+        const char* p = smem + (cp % S16NB) * PANEL16 + tg * 2048 + lane * 16;
+        a.h = *reinterpret_cast<const halfx8*>(p);
+        a.l = *reinterpret_cast<const halfx8*>(p + 1024);
+    };
+    // per element and pair: hi*hi, lo*hi, hi*lo (4 independent accumulators between dependent
+    // MFMAs).  Inline asm with the accumulator constrained to AGPRs at every MFMA: with the
+    // builtin, hipcc renames accumulator tiles between AGPRs and VGPRs inside the loop (v_accvgpr
+    // copies, 48 spilled VGPRs); its waitcnt pass still covers the asm's fragment operands.
+    auto mfma = [&](floatx4& c, const halfx8& a, const halfx8& bq) {
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(bq));
+    };
+    auto mfma_tg = [&](const AF& a, const QF& q, int tg) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) mfma(acc[g][tg], a.h, q.h[g]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) mfma(acc[g][tg], a.l, q.h[g]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) mfma(acc[g][tg], a.h, q.l[g]);
+    };
+#define PHASE __builtin_amdgcn_sched_barrier(0)
+    QF qs[2];
+    AF af[2];
+#pragma unroll
+    for (int k = 0; k < S16NB - 1; ++k) {
+        issue(k);
+        PHASE;
+    }
+    load_q(0, qs[0]);
+    PHASE;
+    wait_vm_n<true>(s16_vm_after(0));   // t(0) landed
+    __builtin_amdgcn_s_barrier();
+    PHASE;
+    read_a(0, 0, af[0]);
+    PHASE;
+#pragma unroll
+    for (int cp = 0; cp < NCP; ++cp) {
+        if (cp + 1 < NCP) load_q(cp + 1, qs[(cp + 1) & 1]);
+        PHASE;
+#pragma unroll
+        for (int tg = 0; tg < 8; ++tg) {
+            if (tg == 6 && cp + 1 < NCP) {   // mid(cp): publish t(cp + 1), retire the reads of t(cp - 1)
+                wait_vm_n<true>(s16_vm_after(cp + 1));
+                __builtin_amdgcn_s_barrier();
+                PHASE;
+                if (cp + S16NB - 1 < NCP) issue(cp + S16NB - 1);
+                if (cp + 2 == NCP) load_exponents();   // after the last static wait
+                PHASE;
+            }
+            if (tg + 1 < 8) read_a(cp, tg + 1, af[(tg + 1) & 1]);
+            else if (cp + 1 < NCP) read_a(cp + 1, 0, af[0]);
+            PHASE;
+            mfma_tg(af[tg & 1], qs[cp & 1], tg);
+            PHASE;
+        }
+    }
+#undef PHASE
+    // the last MFMAs' results are read by v_accvgpr_read in the epilogue: the hazard recognizer does
+    // not see into the asm, so pad the XDL write -> VALU read distance explicitly
+    asm volatile("s_nop 15");
+    asm volatile("s_nop 15");
+    wait_vm<0, true>();   // the exponents have landed and this wave's reads are done ...
+    exq[tid] = eq;
+    if (tid < 128) {
+        ext[tid] = -et;
+        fst[tid] = exp2i(max(-63, min(-et, 63)));
+    }
+    __syncthreads();      // ... in every wave: the panel buffers are the epilogue's scratch
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(acc[g][t]));
+    split16_epilogue<MUL>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
 }
 
 // ============================================================================================
@@ -871,7 +1255,10 @@ __device__ __forceinline__ void split_f16(const float (&v)[8], float s, halfx8& 
     }
 }
 
-template <bool ISB>
+// L16: the panel layout of build_split16_kernel (16 KB per 128-pixel tile and 32-deep chunk pair:
+// [16-pixel group g][hi | lo][k block kb][pixel r][8 halves], k = 8 kb + j within the pair; fmap2
+// positions in split16_target order) instead of build_split_kernel's 8-KB chunk panels.
+template <bool ISB, bool L16>
 __device__ __forceinline__ void pack_body(const float* __restrict__ x, const BuildParams& P, int* __restrict__ ex,
                                           char* __restrict__ pack) {
     __shared__ float red[4][64];
@@ -900,14 +1287,15 @@ __device__ __forceinline__ void pack_body(const float* __restrict__ x, const Bui
             tile = trow * P.n_ntx + (ok ? col : 0);
             y = 2 * r4 + (l >> 5);
             x = l & 15;
-            pos = 64 * (x >> 3) + 32 * (y >> 2) + 8 * (y & 3) + (x & 7);
+            pos = L16 ? 16 * (2 * (y & 3) + ((x >> 2) & 1)) + 4 * ((y >> 2) | ((x >> 3) << 1)) + (x & 3)
+                      : 64 * (x >> 3) + 32 * (y >> 2) + 8 * (y & 3) + (x & 7);
         } else {
             const int bb = blockIdx.x - nreg_blk;
             tile = P.n_reg + (bb >> 1);
             ok = tile < P.n_nt;
             y = 2 * (bb & 1) + (l >> 5);
             x = l & 31;
-            pos = 32 * (x >> 3) + 8 * y + (x & 7);
+            pos = L16 ? 16 * (2 * y + ((x >> 2) & 1)) + 4 * (x >> 3) + (x & 3) : 32 * (x >> 3) + 8 * y + (x & 7);
         }
         const NTile n = ntile_of(P, ok ? tile : 0);
         live = ok;
@@ -943,16 +1331,19 @@ __device__ __forceinline__ void pack_body(const float* __restrict__ x, const Bui
     if (qtr == 0 && pix >= 0) ex[(int64_t)b * N + pix] = e;
     const float s = exp2i(e);
     const int ntiles = ISB ? P.n_nt : P.n_mt;
-    char* pan = pack + ((int64_t)b * ntiles + tile) * dc * PANEL + (pos >> 5) * 2048 + (pos & 31) * 16;
+    char* pan = pack + ((int64_t)b * ntiles + tile) * dc * PANEL +
+                (L16 ? (pos >> 4) * 2048 + (pos & 15) * 16 : (pos >> 5) * 2048 + (pos & 31) * 16);
     auto put = [&](int c, const float (&w)[16]) {
         halfx8 h0, l0, h1, l1;
         split_f16(*reinterpret_cast<const float(*)[8]>(w), s, h0, l0);
         split_f16(*reinterpret_cast<const float(*)[8]>(w + 8), s, h1, l1);
-        char* p = pan + (int64_t)c * PANEL;
+        // L16: chunk c is k blocks 2 (c & 1), 2 (c & 1) + 1 of chunk pair c / 2
+        char* p = L16 ? pan + (int64_t)(c >> 1) * 2 * PANEL + (c & 1) * 512 : pan + (int64_t)c * PANEL;
+        const int k8 = L16 ? 256 : 512;   // the next 8 k
         *reinterpret_cast<halfx8*>(p) = h0;
-        *reinterpret_cast<halfx8*>(p + 512) = h1;
+        *reinterpret_cast<halfx8*>(p + k8) = h1;
         *reinterpret_cast<halfx8*>(p + 1024) = l0;
-        *reinterpret_cast<halfx8*>(p + 1536) = l1;
+        *reinterpret_cast<halfx8*>(p + 1024 + k8) = l1;
     };
     if (!live) return;   // (after the block's only barrier)
     if (regs) {
@@ -976,11 +1367,12 @@ __device__ __forceinline__ void pack_body(const float* __restrict__ x, const Bui
 // tiles), z = 1 fmap2 (n-tiles).  Neither pass alone fills the chip; one grid overlaps the two and
 // drops a launch boundary (round-1 A/B, profiles/r01_final8/ab_pack.txt).  Surplus x blocks of the
 // shorter pass return at once (block-uniform, before pack_body's barrier).
+template <bool L16>
 __global__ __launch_bounds__(256) void pack_both_kernel(BuildParams P) {
     if (blockIdx.z == 0) {
-        if ((int)blockIdx.x < 2 * P.n_mt) pack_body<false>(P.f1, P, P.ex1, const_cast<char*>(P.pk1));
+        if ((int)blockIdx.x < 2 * P.n_mt) pack_body<false, L16>(P.f1, P, P.ex1, const_cast<char*>(P.pk1));
     } else if ((int)blockIdx.x < 4 * (P.n_reg / P.n_ntx) * ((P.n_ntx + 1) / 2) + 2 * (P.n_nt - P.n_reg)) {
-        pack_body<true>(P.f2, P, P.ex2, const_cast<char*>(P.pk2));
+        pack_body<true, L16>(P.f2, P, P.ex2, const_cast<char*>(P.pk2));
     }
 }
 
@@ -1456,15 +1848,20 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
         P.pk2 = P.ws + w.pk2;
         const int nx2 = 4 * (P.n_reg / P.n_ntx) * ((P.n_ntx + 1) / 2) + 2 * (P.n_nt - P.n_reg);   // fmap2 blocks
         const int nx = 2 * P.n_mt > nx2 ? 2 * P.n_mt : nx2;
-        if (stages & 1) hipLaunchKernelGGL(pack_both_kernel, dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
+        // D = 256: build_split16_kernel and its panel layout; other D: build_split_kernel
+        const bool s16 = (P.D + 15) / 16 == 2 * NCP;
+        if (stages & 1) {
+            if (s16) hipLaunchKernelGGL(pack_both_kernel<true>, dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
+            else hipLaunchKernelGGL(pack_both_kernel<false>, dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
+        }
         if (!(stages & 2)) {
             const hipError_t e = hipGetLastError();
             return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
         }
         const dim3 grid((unsigned)ntiles);
-        if ((P.D + 15) / 16 == 16) {
-            if (P.scale_is_mul) hipLaunchKernelGGL((build_split_kernel<true, 16>), grid, dim3(256), 0, stream, P);
-            else hipLaunchKernelGGL((build_split_kernel<false, 16>), grid, dim3(256), 0, stream, P);
+        if (s16) {
+            if (P.scale_is_mul) hipLaunchKernelGGL((build_split16_kernel<true>), grid, dim3(256), 0, stream, P);
+            else hipLaunchKernelGGL((build_split16_kernel<false>), grid, dim3(256), 0, stream, P);
         } else {
             if (P.scale_is_mul) hipLaunchKernelGGL((build_split_kernel<true, 0>), grid, dim3(256), 0, stream, P);
             else hipLaunchKernelGGL((build_split_kernel<false, 0>), grid, dim3(256), 0, stream, P);

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
         int yo[K];
 #pragma unroll
         for (int bb = 0; bb < K; ++bb) yo[bb] = ((int)fy[bb] - org[1]) * SW;
-        const float* wq = st.win + g * SP;
+        const float* wq = st.win + WB::W0 + g * SP;
 #pragma unroll
         for (int ai = 0; ai < AP; ++ai) {
             const int a = part * AP + ai;

@@ -22,8 +22,13 @@ typedef unsigned uint2v __attribute__((ext_vector_type(2)));
 namespace ecorr {
 
 // The staged windows of QB queries and their origins (all phase 1 needs).  PAIR: the window is
-// staged as 8-byte column pairs from an even origin (every level width even), so a staged row
-// holds S + 1 columns.
+// loaded as 8-byte column pairs from the even column at or left of the origin (every level width
+// even) and written into LDS shifted by that one column, so the LDS image starts at the true
+// origin column in both modes: phase 2's offset of sample a from the origin is a (+ a floor flip)
+// for every query, and lanes = queries at the odd stride SP hit distinct banks.  (Unshifted, the
+// even rounding made the offsets a or a + 1 at random across lanes: 49% of the LDS cycles were
+// bank conflicts.)  A staged row holds S + 1 slots in PAIR mode: slot S takes the shifted-out
+// column of odd origins (never read), slot -1 of row 0 the first one (W0 = 1 leading slot).
 template <int R, int QB, bool PAIR = false>
 struct WindowBuf {
     static constexpr int K = 2 * R + 1;   // samples per axis
@@ -31,7 +36,8 @@ struct WindowBuf {
     static constexpr int S = 2 * R + 3;   // staged window side (rows)
     static constexpr int SW = PAIR ? S + 1 : S;   // staged row length
     static constexpr int SP = (S * SW) | 1;       // odd per-query stride: conflict-free lanes = queries
-    float win[QB * SP];
+    static constexpr int W0 = PAIR ? 1 : 0;       // query g's window starts at win[W0 + g SP]
+    float win[W0 + QB * SP];
     // per query: window origin x, y and (mode | needed cols << 8 | needed rows << 16), where mode
     // 0 = staged, 1 = direct gather (coordinates that do not fit the window), 2 = past the range.
     int org[QB][3];
@@ -55,7 +61,6 @@ __device__ __forceinline__ void coord_chain(float cs, int o, float m1, float& f,
 }
 
 // Phase 0b for one query from its first / last x and y floors: origin and mode word (WindowBuf::org).
-// PAIR: the origin column is rounded down to even and the needed columns counted from there.
 template <int S, bool PAIR = false>
 __device__ __forceinline__ void window_origin(bool valid, float x0, float xl, float y0, float yl, int org[3]) {
     int md = 2, X0 = 0, Y0 = 0, NX = 0, NY = 0;
@@ -72,10 +77,6 @@ __device__ __forceinline__ void window_origin(bool valid, float x0, float xl, fl
         // corners span [x0, floor(ix_last) + 1]: monotone round trip, so the last sample bounds it
         NX = ok ? (int)dx + 2 : 0;
         NY = ok ? (int)dy + 2 : 0;
-        if (PAIR) {
-            NX += X0 & 1;   // X0 may be negative: & ~1 rounds toward -inf
-            X0 &= ~1;
-        }
     }
     org[0] = X0;
     org[1] = Y0;
@@ -138,9 +139,11 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB, PAIR>& st, const 
     const float* __restrict__ lvbase = P.lvl[lv] + (ntx < 0 ? g0 * kGroup * hw : R0 * hw);
 
     // ---- phase 1: stage windows, zeros outside the image (grid_sample padding_mode='zeros').
-    // Work item = (query, window column or, PAIR, even column pair); each item walks the S rows.
-    // A pair never straddles the image edge (even origin, even width) and its two floats are
-    // adjacent in every layout (tile rows of 8, block rows of 4 or 2, image rows).  Loads are raw buffer loads
+    // Work item = (query, window column or, PAIR, column pair from the even column xe at or left
+    // of the origin); each item walks the S rows.  A pair never straddles the image edge (even
+    // start, even width) and its two floats are adjacent in every layout (tile rows of 8, block
+    // rows of 4 or 2, image rows); it lands at LDS slots rx - odd, rx - odd + 1 of the row (odd =
+    // origin - xe), so the image starts at the origin.  Loads are raw buffer loads
     // over this group's slab of the level: an element outside the image gets an out-of-range
     // offset and the hardware range check returns 0 -- zero padding with no branch and no select,
     // so all NCOL*S loads of a thread issue back to back.
@@ -167,11 +170,13 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB, PAIR>& st, const 
         const bool live = it < ITEMS;
         const int gq = live ? it / NPX : 0;
         const int rx = (it - gq * NPX) * V;
-        const int x = st.org[gq][0] + rx, y0 = st.org[gq][1], info = st.org[gq][2];
+        const int xo = st.org[gq][0], y0 = st.org[gq][1], info = st.org[gq][2];
+        const int odd = PAIR ? xo & 1 : 0;   // xo may be negative: & 1 / - odd round toward -inf
+        const int x = xo - odd + rx;
         const int ny = (info >> 16) & 0xff;
         // only the needed corner rectangle touches memory; the slack row/column reads 0 for free
-        const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) && (unsigned)x < (unsigned)w;
-        dst[c] = live ? gq * SP + rx : -1;
+        const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) + odd && (unsigned)x < (unsigned)w;
+        dst[c] = live ? WS::W0 + gq * SP + rx - odd : -1;
         // rows ry in [rlo, rhi) are needed and inside the image; the column's byte offset walks
         // down the rows incrementally (tiled: +8 floats inside a tile, + one tile row minus 24 from
         // in-tile row 3; interleaved likewise per block; compact: +w) instead of re-deriving the
@@ -236,7 +241,7 @@ __device__ __forceinline__ float sample_level(const WindowStage<R, QB, PAIR>& st
     const float xa = st.fx[g][a], yb = st.fy[g][bb];
     const float wa = st.wx[g][a], nb = st.wy[g][bb];
     if (md == 0) {
-        const float* c = st.win + g * SP + ((int)yb - st.org[g][1]) * S + ((int)xa - st.org[g][0]);
+        const float* c = st.win + WS::W0 + g * SP + ((int)yb - st.org[g][1]) * S + ((int)xa - st.org[g][0]);
         return blend(c[0], c[1], c[S], c[S + 1], wa, nb);
     }
     return sample_direct(P, lv, b, q0 + g, xa, yb, wa, nb);

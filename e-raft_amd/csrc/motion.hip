@@ -70,7 +70,7 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
         if (md == 0) {   // staged window: origin hoisted, no mode test per sample
             constexpr int K = WS::K, S = WS::SW;   // S: the staged row length
             const int o0 = u.st.org[g][0], o1 = u.st.org[g][1];
-            const float* wq = u.st.win + g * WS::SP;
+            const float* wq = u.st.win + WS::W0 + g * WS::SP;
             // rows of each 16-row block: wave w, half h takes w + 8h and w + 4 + 8h
             for (int k0 = 0; k0 < KK; k0 += 2 * NTM / QBM)
 #pragma unroll

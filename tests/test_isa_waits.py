@@ -1,9 +1,10 @@
 """CPU guard of the build K loops' hand-counted waits.
 
-build_split_kernel<true, 16> and build_f32_kernel<true> (e-raft_amd/csrc/build.hip) stage the
-shared target panel into LDS by LDS-DMA (`buffer_load_dwordx4 ... lds`) through NBUF buffers and
-wait for chunk k with a STATIC `s_waitcnt vmcnt(N)` before barrier k: N counts the VMEM
-instructions the source issues after chunk k's DMA pieces.  That count is right only while hipcc
+build_split16_kernel<true> (the D = 256 split build) and build_f32_kernel<true>
+(e-raft_amd/csrc/build.hip) stage the shared target panel into LDS by LDS-DMA
+(`buffer_load_dwordx4 ... lds`) through NBUF buffers and wait for chunk (pair) k with a STATIC
+`s_waitcnt vmcnt(N)` before barrier k: N counts the VMEM instructions the source issues after
+chunk k's DMA pieces.  That count is right only while hipcc
 keeps the source's issue order (sched_barrier fences hold it today; DESIGN.md §3.1 records the
 hoisted q(0) load that once made barrier 0 release a wave before t(0) landed).
 
@@ -14,9 +15,11 @@ actually emits:
     (vmcnt(N) retires all but the N youngest VMEM instructions; loads, stores and LDS-DMA count
     together, in issue order);
   * WAR: chunk m >= NBUF (which overwrites chunk m - NBUF's buffer) is issued only after barrier
-    m - NBUF + 1, and every barrier is preceded by an lgkmcnt(0) after the wave's last LDS read;
-  * split kernel: the LDS reads between barrier k and k + 1 address buffer k % NBUF (their offset
-    field, one base register).
+    m - NBUF + SPAN (chunk j is read between barriers j and j + SPAN: the split16 loop reads a
+    pair's last target group after the next pair's barrier), and every barrier is preceded by an
+    lgkmcnt(0) after the wave's last LDS read;
+  * split16 kernel: the LDS reads between barrier k and k + 1 address buffers k % NBUF (or
+    (k - 1) % NBUF, SPAN 2) only (their offset field, one base register).
 A deliberately swapped issue order (q(0) hoisted over t(0)) must be flagged.
 """
 import os
@@ -30,11 +33,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "e-raft_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 
-# kernel -> (LDS buffers, DMA pieces per chunk, K chunks, bytes per buffer, query loads per chunk)
+# kernel -> (LDS buffers, DMA pieces per chunk, K chunks, bytes per buffer, query loads per chunk,
+# barriers a chunk's reads span, barriers up to the loop's closing one)
 KERNELS = {
-    "build_split_kernelILb1ELi16EE": dict(nbuf=4, copies=2, nk=16, chunk=8192, qloads=4),
-    "build_f32_kernelILb1EE": dict(nbuf=3, copies=2, nk=16, chunk=8192, qloads=16),
+    "build_split16_kernelILb1EE": dict(nbuf=4, copies=4, nk=8, chunk=16384, qloads=8, span=2, barriers=9),
+    "build_f32_kernelILb1EE": dict(nbuf=3, copies=2, nk=16, chunk=8192, qloads=16, span=1, barriers=18),
 }
+SPLIT = "build_split16_kernelILb1EE"
 
 
 @pytest.fixture(scope="module")
@@ -70,7 +75,7 @@ def is_dma(ln):
     return ln.startswith("buffer_load") and ln.split()[-1] == "lds"
 
 
-def check_loop(ins, nbuf, copies, nk, chunk, check_offsets):
+def check_loop(ins, nbuf, copies, nk, chunk, check_offsets, span=1):
     """Violations of the RAW / WAR rules above (empty list = the waits hold)."""
     errs = []
     issued = done = 0        # VMEM instructions issued / retired (a prefix, in issue order)
@@ -110,8 +115,8 @@ def check_loop(ins, nbuf, copies, nk, chunk, check_offsets):
         errs.append(f"{len(dma)} DMA pieces, not a multiple of {copies}")
     for p, (_, before) in enumerate(dma):
         m = p // copies
-        if m >= nbuf and before < m - nbuf + 2:
-            errs.append(f"chunk {m}'s DMA issued after barrier {before - 1}, before barrier {m - nbuf + 1} "
+        if m >= nbuf and before < m - nbuf + span + 1:
+            errs.append(f"chunk {m}'s DMA issued after barrier {before - 1}, before barrier {m - nbuf + span} "
                         f"retired the reads of chunk {m - nbuf}")
     if check_offsets:
         bases = {re.match(r"ds_read\S*\s+\S+,\s*(\S+)", r).group(1) for _, r in reads}
@@ -121,7 +126,7 @@ def check_loop(ins, nbuf, copies, nk, chunk, check_offsets):
             for region, r in reads:
                 m = re.search(r"offset:(\d+)", r)
                 buf = (int(m.group(1)) if m else 0) // chunk
-                if region < 0 or buf != region % nbuf:
+                if region < 0 or buf not in {(region - d) % nbuf for d in range(span)}:
                     errs.append(f"read in barrier region {region} addresses buffer {buf}: {r}")
     return errs
 
@@ -130,27 +135,27 @@ def check_loop(ins, nbuf, copies, nk, chunk, check_offsets):
 def test_static_waits_match_issue_order(asm, name):
     k = KERNELS[name]
     ins = kernel_loop(asm, name)
-    assert sum(1 for ln in ins if ln == "s_barrier") == k["nk"] + 2
-    assert sum(1 for ln in ins if is_dma(ln)) >= k["copies"] * (k["nk"] + 1)
+    assert sum(1 for ln in ins if ln == "s_barrier") == k["barriers"]
+    assert sum(1 for ln in ins if is_dma(ln)) >= k["copies"] * k["nk"]
     # the query fragment loads (buffer loads to VGPRs; the exponent loads are global_load_dword)
     assert sum(1 for ln in ins if ln.startswith("buffer_load") and not is_dma(ln)) == k["qloads"] * k["nk"]
-    errs = check_loop(ins, k["nbuf"], k["copies"], k["nk"], k["chunk"], name.startswith("build_split"))
+    errs = check_loop(ins, k["nbuf"], k["copies"], k["nk"], k["chunk"], name == SPLIT, k["span"])
     assert not errs, "\n".join(errs)
 
 
 def test_checker_flags_a_hoisted_query_load(asm):
     """q(0) moved in front of t(0) -- the race DESIGN.md §3.1 records -- is caught at barrier 0."""
-    k = KERNELS["build_split_kernelILb1ELi16EE"]
-    ins = kernel_loop(asm, "build_split_kernelILb1ELi16EE")
+    k = KERNELS[SPLIT]
+    ins = kernel_loop(asm, SPLIT)
     first = next(i for i, ln in enumerate(ins) if is_dma(ln))
     q = [i for i, ln in enumerate(ins) if i > first and is_vmem(ln) and not is_dma(ln)][:k["qloads"]]
     swapped = ins[:first] + [ins[i] for i in q] + [ln for i, ln in enumerate(ins[first:], first) if i not in q]
-    errs = check_loop(swapped, k["nbuf"], k["copies"], k["nk"], k["chunk"], True)
+    errs = check_loop(swapped, k["nbuf"], k["copies"], k["nk"], k["chunk"], True, k["span"])
     assert any(e.startswith("barrier 0:") for e in errs), errs
     # and a DMA refill issued one barrier early (WAR on a buffer still being read)
     dmas = [i for i, ln in enumerate(ins) if is_dma(ln)]
     p = dmas[k["copies"] * k["nbuf"]]           # first piece of chunk NBUF
     bar = max(i for i, ln in enumerate(ins[:p]) if ln == "s_barrier")
     early = ins[:bar] + [ins[p]] + [ln for i, ln in enumerate(ins[bar:], bar) if i != p]
-    errs = check_loop(early, k["nbuf"], k["copies"], k["nk"], k["chunk"], True)
+    errs = check_loop(early, k["nbuf"], k["copies"], k["nk"], k["chunk"], True, k["span"])
     assert any("before barrier" in e for e in errs), errs

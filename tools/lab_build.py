@@ -154,12 +154,12 @@ PATCHES["loopprio3"] = [("build.hip", "    TFrags fa, fb;\n", "    __builtin_amd
 # lookup ablations (timing only): no window loads / no output stores / no blends (one LDS read)
 PATCHES["lk_nostage"] = [("lookup_stage.h", "            vals[c][ry] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));",
                           "            vals[c][ry] = (float)(need ? off : 0);")]
-PATCHES["lk_nostore"] = [("lookup.hip", """                const float v = blend(c[0], c[1], c[S], c[S + 1], wx[ai], wy[bb]);
+PATCHES["lk_nostore"] = [("lookup.hip", """                const float v = blend(c[0], c[1], c[SW], c[SW + 1], wx[ai], wy[bb]);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
                                                       sbase + (a * K + bb) * P.q_count * 4, 2);""",
-                          """                const float v = blend(c[0], c[1], c[S], c[S + 1], wx[ai], wy[bb]);
+                          """                const float v = blend(c[0], c[1], c[SW], c[SW + 1], wx[ai], wy[bb]);
                 asm volatile("" :: "v"(v), "v"(sbase + (a * K + bb) * P.q_count * 4));""")]
-PATCHES["lk_noblend"] = [("lookup.hip", "                const float v = blend(c[0], c[1], c[S], c[S + 1], wx[ai], wy[bb]);",
+PATCHES["lk_noblend"] = [("lookup.hip", "                const float v = blend(c[0], c[1], c[SW], c[SW + 1], wx[ai], wy[bb]);",
                           "                const float v = c[0];")]
 # lookup: every staging load issued twice (same bytes, 2x the lane requests): is staging bound by
 # the per-lane request rate?
@@ -260,6 +260,77 @@ PATCHES["stamps4"] = [
     ("build.hip", "    split_epilogue<MUL>(P, acc, smem + wave * (4 * 32 * XS), wave * 64, exq, ext, fst, tc, b, q0, lane);\n}\n\n// ====",
      "    split_epilogue<MUL>(P, acc, smem + wave * (4 * 32 * XS), wave * 64, exq, ext, fst, tc, b, q0, lane);\n    __syncthreads();\n    stamp(2);\n}\n\n// ===="),
     ("build.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + STAMP_EXPORT),
+]
+# split16 kernel: the 32x32 build_split_kernel launched instead (same late exponent loads), for A/B
+PATCHES["s32"] = [("build.hip", "        const bool s16 = (P.D + 15) / 16 == 2 * NCP;", "        const bool s16 = false;")]
+# split16 per-block timing, wave 0 lane 0 -> g_st16[block] = {prologue realtime, loop cycles, loop
+# realtime, epilogue cycles, epilogue realtime, mid-wait+barrier cycles, HW_ID, XCC_ID}
+# (s_memtime cycles, s_memrealtime 10 ns ticks); tools/stamps16.py
+ST16_DECL = """
+__device__ unsigned long long g_st16[65536][8];
+"""
+ST16_EXPORT = """
+extern "C" __attribute__((visibility("default"))) int ecorr_lab_stamps16(void* dst, int n) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ecorr::g_st16), (size_t)n * 64, 0, hipMemcpyDeviceToHost);
+}
+"""
+PATCHES["st16"] = [
+    ("build.hip", "constexpr int SQ = 256; ", ST16_DECL + "constexpr int SQ = 256; "),
+    ("build.hip", """    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int b, qt, nt;
+    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    const NTile tc = ntile_of(P, nt);
+    const int q0 = qt * SQ;
+    const int H = P.H, W = P.W;
+    const int64_t Q = (int64_t)H * W;
+
+    // per-pixel exponents: loaded behind the K loop's last static wait (only the epilogue reads them)""",
+     """    const unsigned long long r_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long c_mid = 0;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int b, qt, nt;
+    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    const NTile tc = ntile_of(P, nt);
+    const int q0 = qt * SQ;
+    const int H = P.H, W = P.W;
+    const int64_t Q = (int64_t)H * W;
+
+    // per-pixel exponents: loaded behind the K loop's last static wait (only the epilogue reads them)"""),
+    ("build.hip", """    wait_vm_n<true>(s16_vm_after(0));   // t(0) landed
+    __builtin_amdgcn_s_barrier();
+    PHASE;""", """    wait_vm_n<true>(s16_vm_after(0));   // t(0) landed
+    __builtin_amdgcn_s_barrier();
+    PHASE;
+    const unsigned long long c_loop0 = __builtin_amdgcn_s_memtime(), r_loop0 = __builtin_amdgcn_s_memrealtime();
+    PHASE;"""),
+    ("build.hip", """            if (tg == 6 && cp + 1 < NCP) {   // mid(cp): publish t(cp + 1), retire the reads of t(cp - 1)
+                wait_vm_n<true>(s16_vm_after(cp + 1));
+                __builtin_amdgcn_s_barrier();
+                PHASE;""", """            if (tg == 6 && cp + 1 < NCP) {   // mid(cp): publish t(cp + 1), retire the reads of t(cp - 1)
+                const unsigned long long cm = __builtin_amdgcn_s_memtime();
+                wait_vm_n<true>(s16_vm_after(cp + 1));
+                __builtin_amdgcn_s_barrier();
+                c_mid += __builtin_amdgcn_s_memtime() - cm;
+                PHASE;"""),
+    ("build.hip", """    __syncthreads();      // ... in every wave: the panel buffers are the epilogue's scratch""",
+     """    __syncthreads();      // ... in every wave: the panel buffers are the epilogue's scratch
+    const unsigned long long c_loop1 = __builtin_amdgcn_s_memtime(), r_loop1 = __builtin_amdgcn_s_memrealtime();"""),
+    ("build.hip", """    split16_epilogue<MUL>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+}""", """    split16_epilogue<MUL>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+    __syncthreads();
+    if (tid == 0 && blockIdx.x < 65536) {
+        unsigned long long* g = g_st16[blockIdx.x];
+        g[0] = r_loop0 - r_start;
+        g[1] = c_loop1 - c_loop0;
+        g[2] = r_loop1 - r_loop0;
+        g[3] = __builtin_amdgcn_s_memtime() - c_loop1;
+        g[4] = __builtin_amdgcn_s_memrealtime() - r_loop1;
+        g[5] = c_mid;
+        g[6] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+        g[7] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+    }
+}"""),
+    ("build.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + ST16_EXPORT),
 ]
 # the tree as it is (the baseline of an A/B against an edited tree)
 PATCHES["base"] = []
