@@ -48,7 +48,7 @@ def asm():
         pytest.skip("hipcc not installed")
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "build.s")
-        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
                         "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S",
                         os.path.join(CSRC, "build.hip"), "-o", out],
                        check=True, capture_output=True)

@@ -263,8 +263,8 @@ PATCHES["stamps4"] = [
 ]
 # split16 kernel: the 32x32 build_split_kernel launched instead (same late exponent loads), for A/B
 PATCHES["s32"] = [("build.hip", "        const bool s16 = (P.D + 15) / 16 == 2 * NCP;", "        const bool s16 = false;")]
-# split16 per-block timing, wave 0 lane 0 -> g_st16[block] = {prologue realtime, loop cycles, loop
-# realtime, epilogue cycles, epilogue realtime, mid-wait+barrier cycles, HW_ID, XCC_ID}
+# split16 per-block timing, lane 0 of wave 0 -> g_st16[block] = {start, loop start, loop end, block end
+# (s_memrealtime), loop cycles, epilogue cycles (s_memtime), HW_ID, XCC_ID}
 # (s_memtime cycles, s_memrealtime 10 ns ticks); tools/stamps16.py
 ST16_DECL = """
 __device__ unsigned long long g_st16[65536][8];
@@ -320,18 +320,23 @@ PATCHES["st16"] = [
     __syncthreads();
     if (tid == 0 && blockIdx.x < 65536) {
         unsigned long long* g = g_st16[blockIdx.x];
-        g[0] = r_loop0 - r_start;
-        g[1] = c_loop1 - c_loop0;
-        g[2] = r_loop1 - r_loop0;
-        g[3] = __builtin_amdgcn_s_memtime() - c_loop1;
-        g[4] = __builtin_amdgcn_s_memrealtime() - r_loop1;
-        g[5] = c_mid;
+        g[0] = r_start;
+        g[1] = r_loop0;
+        g[2] = r_loop1;
+        g[3] = __builtin_amdgcn_s_memrealtime();
+        g[4] = c_loop1 - c_loop0;
+        g[5] = __builtin_amdgcn_s_memtime() - c_loop1;
+        (void)c_mid;
         g[6] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
         g[7] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
     }
 }"""),
     ("build.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + ST16_EXPORT),
 ]
+# split16 epilogue stores issued out of range (timing only: same instructions, no store traffic)
+PATCHES["e16oob"] = [("build.hip", "lok && qloc < nq ? (int)(qloc * P.lsz[0] * 4) + loff : SOOB, 0,", "SOOB, 0,"),
+                     ("build.hip", "        const bool in = on && qloc < nq && by < P.lnty[lv] && bx < -P.lntx[lv];",
+                      "        const bool in = false && on && qloc < nq && by < P.lnty[lv] && bx < -P.lntx[lv];")]
 # the tree as it is (the baseline of an A/B against an edited tree)
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
@@ -392,6 +397,7 @@ COMBOS.update({"loopstamps_qwait": ["loopstamps", "qwait"]})
 COMBOS.update({"stamps_epi_noscale": ["stamps", "epi_noscale"], "stamps_epi_nolds": ["stamps", "epi_nolds"]})
 COMBOS.update({"sameqt": ["sameq", "samet"]})
 COMBOS.update({"dmaqoob": ["dmaoob", "qoob"], "noepi_r2": ["noepi"]})
+COMBOS.update({"st16_e16oob": ["st16", "e16oob"]})
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"], "loopstamps_noepi_mfma16": ["loopstamps", "noepi", "mfma16"]})
 
 
