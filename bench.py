@@ -17,7 +17,8 @@ One step = one pass of the hot path over one batch: CorrBlock build (split-f16 o
     python bench.py [--gpus N --steps K --warmup W --batch 16 --no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 
-Prints ONE JSON line on rank 0 with `roofline` (the dominant kernel, build_split_kernel alone,
+Prints ONE JSON line on rank 0 with `roofline` (the dominant kernel, the split GEMM alone --
+build_split16_kernel at D = 256 --
 HIP events on its launch stream inside the timed region; `window_frac` = the whole build with its
 operand pass; `traffic` = PMC HBM bytes from profiles/latest_pmc.json when its source digest
 matches this tree), `kernels` (build, pack, lookup, build_fp32) and `cpu_baseline` (SURVEY 8(d):
@@ -553,15 +554,17 @@ def main():
 
     look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
     kernels = {}
+    # the split GEMM kernel: v_mfma_f32_16x16x32_f16 at D = 256 (E-RAFT), the 32x32x16 kernel otherwise
+    split_kernel = "build_split16_kernel" if D == 256 else "build_split_kernel"
     if mode == "split":
         bind, other = roofs(gemm_ms)
         wbind, _ = roofs(build_ms)
         kernels["build"] = dict(bind, ms_per_launch=round(gemm_ms, 4), mode=mode,
-                                covers="build_split_kernel alone (GEMM + fused pyramid; HIP events on the launch stream "
+                                covers=f"{split_kernel} alone (GEMM + fused pyramid; HIP events on the launch stream "
                                        "around its launch inside the timed region)",
                                 other_roof={k: other[k] for k in ("bound", "achieved", "peak", "unit", "frac")},
                                 window={"ms": round(build_ms, 4), "frac": wbind["frac"], "achieved": wbind["achieved"],
-                                        "covers": "pack_both_kernel + build_split_kernel (the whole CorrBlock build)"})
+                                        "covers": f"pack_both_kernel + {split_kernel} (the whole CorrBlock build)"})
         kernels["pack"] = {"ms_per_launch": round(pack_ms, 4), "covers": "pack_both_kernel (operand pass)",
                            "bound": "hbm", "work_per_launch": f"{4.0 * B * D * (q_local + H * W) * 2:.4g} B "
                                                              "(fmaps in, f16 hi/lo panels out)"}
@@ -577,7 +580,7 @@ def main():
             kernels["build_fp32"] = measure_fp32_build(f1, f2)
     dom = "build" if gemm_ms >= look_ms * iters else "lookup"
     roof = {k: kernels[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")}
-    roof["kernel"] = "build_split_kernel" if (dom == "build" and mode == "split") else \
+    roof["kernel"] = split_kernel if (dom == "build" and mode == "split") else \
         ("build_kernel" if dom == "build" else "lookup_cols_reg")
     if dom == "build" and mode == "split":
         roof["window_frac"] = kernels["build"]["window"]["frac"]
@@ -587,7 +590,7 @@ def main():
     roof["traffic"] = traffic
     roof["traffic_source"] = src
     ideal_s = max(t_mfma, t_hbm) + iters * look_bytes / (PEAK_HBM_GBS * 1e9)
-    if a.mode == "batch":
+    if a.mode == "batch" and not a.no_next:
         with torch.no_grad():
             kernels.update(measure_lookup_fields(make_block(), B, H, W, iters, look_bytes, device))
     if mode == "split" and a.mode == "batch" and world == 1 and not a.no_next:

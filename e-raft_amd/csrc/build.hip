@@ -310,9 +310,11 @@ __device__ __forceinline__ void split_epilogue(const BuildParams& P, floatx16 (&
                     for (int g4 = 0; g4 < 4; ++g4) {
                         const floatx4 s4 = *reinterpret_cast<const floatx4*>(fst + 32 * j + 8 * g4 + 4 * arow);
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const float x = __fmul_rn(acc[i][j][4 * g4 + t], __fmul_rn(sq, s4[t]));
-                            v[jl][g4][t] = MUL ? x : __fdiv_rn(x, P.scale);
+                        for (int h = 0; h < 2; ++h) {   // exact power-of-two products, v_pk_mul_f32 pairs
+                            const floatx2 x = floatx2{acc[i][j][4 * g4 + 2 * h], acc[i][j][4 * g4 + 2 * h + 1]} *
+                                              (floatx2{sq, sq} * floatx2{s4[2 * h], s4[2 * h + 1]});
+                            v[jl][g4][2 * h] = MUL ? x[0] : __fdiv_rn(x[0], P.scale);
+                            v[jl][g4][2 * h + 1] = MUL ? x[1] : __fdiv_rn(x[1], P.scale);
                         }
                     }
                 }
@@ -749,7 +751,10 @@ static_assert(S16NB != 4 || S16COPIES != 4 || S16QL != 8 ||
 
 // Epilogue of build_split16_kernel for one wave: its 64 queries (block-local qw .. qw + 63) x the
 // n-tile tc from its accumulators acc[qg][tg]; xw = the wave's two LDS transpose regions (2 x 64
-// lines x S16LS bytes).
+// lines x S16LS bytes).  It runs beside the partner block's K loop, whose MFMAs hold the SIMD's
+// vector issue half the time, so its VALU count is the cost: every address is 32-bit and hoisted
+// out of the query-group loop (the quadrant geometry is the lane's; only the query row changes),
+// and the cross-lane steps are v_permlane16/32_swap.
 template <bool MUL>
 __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (&acc)[4][8], char* const xw, int qw,
                                                  const int* exq, const int* ext, const float* fst, const NTile& tc,
@@ -786,25 +791,40 @@ __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (
         pc = g1 ? (second ? (l < 20 ? l - 16 : l - 24) : l - 4) : (second ? l - 20 : (l < 4 ? l : l - 8));
         jl = 4 * (lane >> 5) + 2 * (g1 ? 1 : 0) + (second ? 1 : 0);
     }
-    const int lq = jl & 1 ? 8 : 0, lk = jl >> 1;   // line s + 8 jl: query s + lq, quadrant lk
-    const int ltr = line_tr(lk), ltc = line_tc(lk);
-    const bool lok = ltr < P.lnty[0] && ltc < P.lntx[0];
-    const int loff = ((ltr * P.lntx[0] + ltc) * kTile) * 4 + 16 * pc;
-    // One interleaved-level piece: query qloc (block-local), level pixel (r, c), N floats in a row.
-    // Queries past the block and blocks outside the level are dropped.
-    auto store_px = [&](__amdgpu_buffer_rsrc_t rs, int lv, int qloc, int r, int c, auto val, bool on) {
-        constexpr int N = sizeof(val) / 4;
+    const int l0stride = (int)P.lsz[0] * 4;            // bytes per query image
+    int l0off;                                          // this lane's piece of line s + 8 jl, query row qw + s (+ lq)
+    bool l0ok;
+    {
+        const int lk = jl >> 1, ltr = line_tr(lk), ltc = line_tc(lk);
+        l0ok = ltr < P.lnty[0] && ltc < P.lntx[0];
+        l0off = (qw + (jl & 1 ? 8 : 0)) * l0stride + ((ltr * P.lntx[0] + ltc) * kTile) * 4 + 16 * pc;
+    }
+    const int l0q = qw + (jl & 1 ? 8 : 0);              // query row of store s = 0 (block-local)
+    // Interleaved levels 1-3 ([group][block][row][bh][bw], ecorr_device.h): a piece of query row R
+    // (block-local qloc) at byte (grp G + rin bsz + blkoff) 4, grp = (R >> 6) - g0, rin = R & 63,
+    // G = kGroup lsz floats per group, bsz = block floats; blkoff = block index kGroup bsz + the
+    // piece's in-block offset (the lane's; -1 = outside the level)
+    const int rl0 = (int)(rows0 & (kGroup - 1));          // row-in-group of the block's first query
+    auto ilv_blkoff = [&](int lv, int r, int c) {          // level pixel (r, c) -> blkoff, or -1
         const int sy = ilv_sy(lv), sx = ilv_sx(lv);
         const int by = r >> sy, bx = c >> sx;
-        const bool in = on && qloc < nq && by < P.lnty[lv] && bx < -P.lntx[lv];
-        const int64_t R = rows0 + qloc;
-        const int off = (int)((((R >> 6) - g0) * kGroup * P.lsz[lv] +
-                               ((int64_t)(by * -P.lntx[lv] + bx) * kGroup + (R & (kGroup - 1))) * (1 << (sy + sx)) +
-                               ((r & ((1 << sy) - 1)) << sx) + (c & ((1 << sx) - 1))) * 4);
-        if constexpr (N == 4)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, val), rs, in ? off : SOOB, 0, ST_L01);
-        else
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, val), rs, in ? off : SOOB, 0, ST_L01);
+        if (by >= P.lnty[lv] || bx >= -P.lntx[lv]) return -1;
+        return (by * -P.lntx[lv] + bx) * kGroup * (1 << (sy + sx)) + ((r & ((1 << sy) - 1)) << sx) + (c & ((1 << sx) - 1));
+    };
+    // level 1: after the row swap, lane kb holds block row kb & 1 of quadrants kb & ~1 (x) and kb | 1 (y)
+    const int b1x = L > 1 ? ilv_blkoff(1, 2 * line_tr(kb & ~1) + (kb & 1), 4 * line_tc(kb & ~1)) : -1;
+    const int b1y = L > 1 ? ilv_blkoff(1, 2 * line_tr(kb | 1) + (kb & 1), 4 * line_tc(kb | 1)) : -1;
+    // level 2: the quadrant's 1 x 2 pixels at (line_tr, 2 line_tc)
+    const int b2 = L > 2 ? ilv_blkoff(2, line_tr(kb), 2 * line_tc(kb)) : -1;
+    // level 3 (regular tiles, stored by the kb = 0 lanes): the tile's 1 x 2 at (ty0 / 8, tx0 / 8)
+    const int b3 = (L > 3 && !tc.band && kb == 0) ? ilv_blkoff(3, tc.ty0 >> 3, tc.tx0 >> 3) : -1;
+    const int G1 = kGroup * (int)P.lsz[L > 1 ? 1 : 0], G2 = kGroup * (int)P.lsz[L > 2 ? 2 : 0],
+              G3 = kGroup * (int)P.lsz[L > 3 ? 3 : 0];
+    auto st4 = [&](__amdgpu_buffer_rsrc_t rs, int off, bool ok, floatx4 v) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), rs, ok ? off : SOOB, 0, ST_L01);
+    };
+    auto st2 = [&](__amdgpu_buffer_rsrc_t rs, int off, bool ok, floatx2 v) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, ok ? off : SOOB, 0, ST_L01);
     };
     // fast scale: every exponent of the wave's queries and of the panel's targets in [-63, 63]
     bool fast_scale;
@@ -820,14 +840,20 @@ __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (
         // v[tg][i] = quadrant pixel (tg >> 1, 4 (tg & 1) + i) of query ql + qn, quadrant kb
         float v[8][4];
         if (fast_scale) {
+            // x = acc 2^nqe 2^ext: exact power-of-two products, as v_pk_mul_f32 pairs (the
+            // library is built without SLP vectorization, which packed the pooling adds at two
+            // v_mov each; packing is spelled out where it pays)
             const float sq = exp2i(nqe);
+            const floatx2 sq2 = {sq, sq};
 #pragma unroll
             for (int tg = 0; tg < 8; ++tg) {
                 const floatx4 s4 = *reinterpret_cast<const floatx4*>(fst + 16 * tg + 4 * kb);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float x = __fmul_rn(acc[qg][tg][i], __fmul_rn(sq, s4[i]));
-                    v[tg][i] = MUL ? x : __fdiv_rn(x, P.scale);
+                for (int h = 0; h < 2; ++h) {
+                    const floatx2 x = floatx2{acc[qg][tg][2 * h], acc[qg][tg][2 * h + 1]} *
+                                      (sq2 * floatx2{s4[2 * h], s4[2 * h + 1]});
+                    v[tg][2 * h] = MUL ? x[0] : __fdiv_rn(x[0], P.scale);
+                    v[tg][2 * h + 1] = MUL ? x[1] : __fdiv_rn(x[1], P.scale);
                 }
             }
         } else {
@@ -849,14 +875,14 @@ __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (
         for (int tg = 0; tg < 8; ++tg)
             *reinterpret_cast<floatx4*>(xr + lane * S16LS + 16 * tg) = floatx4{v[tg][0], v[tg][1], v[tg][2], v[tg][3]};
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const floatx4 pcv = *reinterpret_cast<const floatx4*>(xr + (s + 8 * jl) * S16LS + 16 * pc);
-            const int qloc = ql + s + lq;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, pcv), r0,
-                                                   lok && qloc < nq ? (int)(qloc * P.lsz[0] * 4) + loff : SOOB, 0,
-                                                   ST_L01);
-        }
+        for (int s = 0; s < 8; ++s)
+            st4(r0, l0off + (16 * qg + s) * l0stride, l0ok && l0q + 16 * qg + s < nq,
+                *reinterpret_cast<const floatx4*>(xr + (s + 8 * jl) * S16LS + 16 * pc));
         if (L < 2) continue;
+        // this lane's query row in its interleaved group
+        const int rr = rl0 + ql + qn;
+        const int grp = rr >> 6, rin = rr & (kGroup - 1);
+        const bool qok = ql + qn < nq;
         // level 1: the quadrant's 2 x 4 block, l1[r][c] from quadrant rows 2r, 2r + 1, cols 2c, 2c + 1
         auto q0v = [&](int yy, int xx) { return v[2 * yy + (xx >> 2)][xx & 3]; };
         float l1[2][4];
@@ -864,41 +890,39 @@ __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (
         for (int r = 0; r < 2; ++r)
 #pragma unroll
             for (int c = 0; c < 4; ++c)
-                l1[r][c] = pool4_v(q0v(2 * r, 2 * c), q0v(2 * r, 2 * c + 1), q0v(2 * r + 1, 2 * c), q0v(2 * r + 1, 2 * c + 1));
+                l1[r][c] = pool4(q0v(2 * r, 2 * c), q0v(2 * r, 2 * c + 1), q0v(2 * r + 1, 2 * c), q0v(2 * r + 1, 2 * c + 1));
         float l2[2];
         if (L >= 3) {
 #pragma unroll
-            for (int c = 0; c < 2; ++c) l2[c] = pool4_v(l1[0][2 * c], l1[0][2 * c + 1], l1[1][2 * c], l1[1][2 * c + 1]);
+            for (int c = 0; c < 2; ++c) l2[c] = pool4(l1[0][2 * c], l1[0][2 * c + 1], l1[1][2 * c], l1[1][2 * c + 1]);
         }
         // level-1 stores: one swap of 16-lane rows (kb odd rows <-> kb even rows) leaves lane kb with
-        // block-row kb & 1 of the blocks of quadrants kb & ~1 (x) and kb | 1 (y): per instruction,
+        // block row kb & 1 of the blocks of quadrants kb & ~1 (x) and kb | 1 (y): per instruction,
         // 16 queries x 32 B contiguous per block, two blocks
         {
             float x[4], y[4];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                x[c] = l1[0][c];
-                y[c] = l1[1][c];
-                const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[c]), __float_as_uint(y[c]), false, false);
+                const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(l1[0][c]), __float_as_uint(l1[1][c]), false, false);
                 x[c] = __uint_as_float(sw[0]);
                 y[c] = __uint_as_float(sw[1]);
             }
-            const int ke = kb & ~1, ko = kb | 1;
-            // block (ty0 / 4 + ..., tx0 / 8 + ...) of quadrant k at level 1; the lane's block row kb & 1
-            store_px(r1, 1, ql + qn, 2 * (line_tr(ke)) + (kb & 1), 4 * line_tc(ke), floatx4{x[0], x[1], x[2], x[3]}, true);
-            store_px(r1, 1, ql + qn, 2 * (line_tr(ko)) + (kb & 1), 4 * line_tc(ko), floatx4{y[0], y[1], y[2], y[3]}, true);
+            const int base1 = grp * G1 + rin * 8;
+            st4(r1, (base1 + b1x) * 4, qok && b1x >= 0, floatx4{x[0], x[1], x[2], x[3]});
+            st4(r1, (base1 + b1y) * 4, qok && b1y >= 0, floatx4{y[0], y[1], y[2], y[3]});
         }
         if (L < 3) continue;
-        // level 2: the quadrant's 1 x 2 pixels, row ty0 / 4 + (kb & 1) (band: ty0 / 4), cols tx0 / 4 +
-        // 2 (kb >> 1) (band: + 2 kb): 4 lanes x 8 B = one query's 2 x 4 block (band: half of two)
-        store_px(r2, 2, ql + qn, line_tr(kb), 2 * line_tc(kb), floatx2{l2[0], l2[1]}, true);
+        // level 2: 4 lanes x 8 B = one query's 2 x 4 block (band: half of two)
+        st2(r2, (grp * G2 + rin * 8 + b2) * 4, qok && b2 >= 0, floatx2{l2[0], l2[1]});
         if (L < 4 || tc.band) continue;
         // level 3 (regular tiles): pixel kb >> 1 of the tile's 1 x 2 from the 2 x 2 level-2 pixels of
-        // lanes kb (row 0, kb even) and kb + 1 (row 1); lane kb = 0 stores both pixels
-        const float o0 = __shfl_xor(l2[0], 16), o1 = __shfl_xor(l2[1], 16);
-        const float p3 = pool4_v(l2[0], l2[1], o0, o1);
-        const float p3b = __shfl_xor(p3, 32);   // lane kb = 0 <- kb = 2
-        store_px(r3, 3, ql + qn, tc.ty0 >> 3, tc.tx0 >> 3, floatx2{p3, p3b}, kb == 0);
+        // lanes kb (row 0, kb even) and kb + 1 (row 1), brought over by a row swap; lane kb = 0 takes
+        // pixel 1 from kb = 2 by a half swap and stores both
+        const auto o0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l2[0]), __float_as_uint(l2[0]), false, false);
+        const auto o1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l2[1]), __float_as_uint(l2[1]), false, false);
+        const float p3 = pool4(l2[0], l2[1], __uint_as_float(o0[1]), __uint_as_float(o1[1]));
+        const auto p3s = __builtin_amdgcn_permlane32_swap(__float_as_uint(p3), __float_as_uint(p3), false, false);
+        st2(r3, (grp * G3 + rin * 2 + b3) * 4, qok && b3 >= 0, floatx2{p3, __uint_as_float(p3s[1])});
     }
 }
 
@@ -957,7 +981,7 @@ __global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(acc[g][t]));
+        for (int t = 0; t < 8; ++t) asm volatile("" : "+v"(acc[g][t]));
 
     // query fragments of the wave's 4 groups (panel wave / 2, 16-query groups 4 (wave & 1) + g), one pair
     struct QF { halfx8 h[4], l[4]; };
@@ -977,11 +1001,13 @@ __global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
         a.l = *reinterpret_cast<const halfx8*>(p + 1024);
     };
     // per element and pair: hi*hi, lo*hi, hi*lo (4 independent accumulators between dependent
-    // MFMAs).  Inline asm with the accumulator constrained to AGPRs at every MFMA: with the
-    // builtin, hipcc renames accumulator tiles between AGPRs and VGPRs inside the loop (v_accvgpr
-    // copies, 48 spilled VGPRs); its waitcnt pass still covers the asm's fragment operands.
+    // MFMAs).  Inline asm with the accumulator constrained to VGPRs at every MFMA (gfx950's
+    // register file is unified: 128 accumulator VGPRs + the loop's ~100 fit the 256 of two waves
+    // per SIMD, and the epilogue's VALU then reads them without 128 v_accvgpr_read per wave); with
+    // the builtin, hipcc renames accumulator tiles between AGPRs and VGPRs inside the loop
+    // (v_accvgpr copies, 48 spilled VGPRs).  Its waitcnt pass still covers the fragment operands.
     auto mfma = [&](floatx4& c, const halfx8& a, const halfx8& bq) {
-        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(bq));
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(bq));
     };
     auto mfma_tg = [&](const AF& a, const QF& q, int tg) {
 #pragma unroll
@@ -1028,8 +1054,8 @@ __global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
         }
     }
 #undef PHASE
-    // the last MFMAs' results are read by v_accvgpr_read in the epilogue: the hazard recognizer does
-    // not see into the asm, so pad the XDL write -> VALU read distance explicitly
+    // the last MFMAs' results are read by the epilogue's VALU: the hazard recognizer does not see
+    // into the asm, so pad the XDL write -> VALU read distance explicitly
     asm volatile("s_nop 15");
     asm volatile("s_nop 15");
     wait_vm<0, true>();   // the exponents have landed and this wave's reads are done ...
@@ -1042,7 +1068,7 @@ __global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(acc[g][t]));
+        for (int t = 0; t < 8; ++t) asm volatile("" : "+v"(acc[g][t]));
     split16_epilogue<MUL>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
 }
 
@@ -1285,7 +1311,9 @@ __device__ __forceinline__ void pack_body(const float* __restrict__ x, const Bui
             const int r4 = blockIdx.x & 3, pr = blockIdx.x >> 2, trow = pr / npair, col = 2 * (pr - trow * npair) + (l >> 4 & 1);
             ok = col < P.n_ntx;
             tile = trow * P.n_ntx + (ok ? col : 0);
-            y = 2 * r4 + (l >> 5);
+            // L16: rows r4, r4 + 4, whose 16 pixels per n-tile row half complete two 16-position
+            // groups of the panel (256-byte runs per store); otherwise rows 2 r4, 2 r4 + 1
+            y = L16 ? r4 + 4 * (l >> 5) : 2 * r4 + (l >> 5);
             x = l & 15;
             pos = L16 ? 16 * (2 * (y & 3) + ((x >> 2) & 1)) + 4 * ((y >> 2) | ((x >> 3) << 1)) + (x & 3)
                       : 64 * (x >> 3) + 32 * (y >> 2) + 8 * (y & 3) + (x & 7);

@@ -337,6 +337,54 @@ PATCHES["st16"] = [
 PATCHES["e16oob"] = [("build.hip", "lok && qloc < nq ? (int)(qloc * P.lsz[0] * 4) + loff : SOOB, 0,", "SOOB, 0,"),
                      ("build.hip", "        const bool in = on && qloc < nq && by < P.lnty[lv] && bx < -P.lntx[lv];",
                       "        const bool in = false && on && qloc < nq && by < P.lnty[lv] && bx < -P.lntx[lv];")]
+# split16 wave priority: the K loop at s_setprio 1 over the partner block's epilogue (the older wave
+# otherwise wins the SIMD's issue arbitration) / the epilogue at 1
+PATCHES["prio_loop"] = [("build.hip", """    read_a(0, 0, af[0]);
+    PHASE;
+#pragma unroll
+    for (int cp = 0; cp < NCP; ++cp) {""", """    read_a(0, 0, af[0]);
+    __builtin_amdgcn_s_setprio(1);
+    PHASE;
+#pragma unroll
+    for (int cp = 0; cp < NCP; ++cp) {"""),
+    ("build.hip", """    wait_vm<0, true>();   // the exponents have landed and this wave's reads are done ...""",
+     """    __builtin_amdgcn_s_setprio(0);
+    wait_vm<0, true>();   // the exponents have landed and this wave's reads are done ...""")]
+PATCHES["prio_epi"] = [("build.hip", """    wait_vm<0, true>();   // the exponents have landed and this wave's reads are done ...""",
+     """    __builtin_amdgcn_s_setprio(1);
+    wait_vm<0, true>();   // the exponents have landed and this wave's reads are done ...""")]
+# split16 epilogue without its level-0 LDS transpose (timing only: each lane stores its own
+# values as the pieces): does the transpose's LDS traffic slow the partner block's K loop?
+PATCHES["e16nolds"] = [("build.hip", """#pragma unroll
+        for (int tg = 0; tg < 8; ++tg)
+            *reinterpret_cast<floatx4*>(xr + lane * S16LS + 16 * tg) = floatx4{v[tg][0], v[tg][1], v[tg][2], v[tg][3]};
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            st4(r0, l0off + (16 * qg + s) * l0stride, l0ok && l0q + 16 * qg + s < nq,
+                *reinterpret_cast<const floatx4*>(xr + (s + 8 * jl) * S16LS + 16 * pc));""", """        (void)xr;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            st4(r0, l0off + (16 * qg + s) * l0stride, l0ok && l0q + 16 * qg + s < nq,
+                floatx4{v[s][0], v[s][1], v[s][2], v[s][3]});""")]
+# split16 K loop alone (timing only): the epilogue replaced by one store of the accumulator sum;
+# and the same with one block per CU (LDS padded past half the CU), i.e. one wave per SIMD
+PATCHES["noepi16"] = [("build.hip", """    split16_epilogue<MUL>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+}""", """    {
+        float sacc = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sacc += acc[g][t][r];
+        P.lvl[0][(int64_t)blockIdx.x * 256 + tid] = sacc;
+    }
+}""")]
+PATCHES["onecu16"] = [("build.hip", """__global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
+    // ALL LDS in this one array (cdna_hip_programming.md trap 4(a), see build_split_kernel)
+    __shared__ __attribute__((aligned(16))) char smem[SLDS + (SQ + 256) * 4];""", """__global__ __launch_bounds__(256, 1) void build_split16_kernel(BuildParams P) {
+    // ALL LDS in this one array (cdna_hip_programming.md trap 4(a), see build_split_kernel)
+    __shared__ __attribute__((aligned(16))) char smem[SLDS + (SQ + 256) * 4 + 16384];""")]
 # the tree as it is (the baseline of an A/B against an edited tree)
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
@@ -397,7 +445,8 @@ COMBOS.update({"loopstamps_qwait": ["loopstamps", "qwait"]})
 COMBOS.update({"stamps_epi_noscale": ["stamps", "epi_noscale"], "stamps_epi_nolds": ["stamps", "epi_nolds"]})
 COMBOS.update({"sameqt": ["sameq", "samet"]})
 COMBOS.update({"dmaqoob": ["dmaoob", "qoob"], "noepi_r2": ["noepi"]})
-COMBOS.update({"st16_e16oob": ["st16", "e16oob"]})
+COMBOS.update({"noepi16_1cu": ["noepi16", "onecu16"]})
+COMBOS.update({"st16_e16oob": ["st16", "e16oob"], "st16_e16nolds": ["st16", "e16nolds"], "st16_prio_loop": ["st16", "prio_loop"]})
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"], "loopstamps_noepi_mfma16": ["loopstamps", "noepi", "mfma16"]})
 
 

@@ -79,7 +79,7 @@ for key in sorted(agg):
         avg = {c: sum(v) / len(v) for c, v in d.items()}
         for c, v in sorted(avg.items()):
             lines.append(f"  {c:28s} {v:16.1f}   (n={len(d[c])})")
-        wide = k.startswith(("build_kernel", "build_split_kernel", "build_f32_kernel"))
+        wide = k.startswith(("build_kernel", "build_split_kernel", "build_split16_kernel", "build_f32_kernel"))
         rec = {"counters": avg}
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
             rd = avg["FETCH_SIZE"] * 1024 * (2 if wide else 1)
