@@ -870,6 +870,8 @@ __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (
         }
         // level 0: the line through the region (a wave's LDS accesses are processed in order, so
         // group qg + 2's writes cannot overtake group qg's reads of the same region)
+        // (stored straight from the lanes instead -- 16-byte pieces of 64 lines per instruction --
+        // the same pyramid took 4.8 ms and wrote 5.4 GB: profiles/r03_lab/r3h_*)
         char* const xr = xw + (qg & 1) * (64 * S16LS);
 #pragma unroll
         for (int tg = 0; tg < 8; ++tg)

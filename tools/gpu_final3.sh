@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round-3 final: every GPU test, smoke, the headline bench + C3 / C5 lines, a 2-rank batch-sharded
+# rehearsal on one GPU (gloo), then the rocprof kernel trace and the PMC passes (C2 full set, C3 /
+# C5 traffic).  usage: tools/gpu_final3.sh TAG
+cd "$GRAFT_REPO_ROOT"; TAG=${1:-r3final}; OUT=gpurun_out/$TAG; mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E 'FAILED|ERROR|passed|failed' $OUT/pytest_gpu.log | tail -8; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -1 $OUT/smoke.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python -u bench.py --batch 64 --height 32 --width 32 --steps 20 --warmup 5 --no-cpu-baseline --no-next > $OUT/bench_c3.log 2>&1
+rc=$?; echo "c3 rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python -u bench.py --mode rowshard --steps 10 --warmup 3 --no-cpu-baseline --no-next > $OUT/bench_c5.log 2>&1
+rc=$?; echo "c5 rc=$rc"; [ $rc -ne 0 ] && exit $rc
+BENCH_SINGLE_DEVICE=1 timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline --no-next > $OUT/bench_2rank.log 2>&1
+rc=$?; echo "2-rank rc=$rc"; [ $rc -ne 0 ] && exit $rc
+python3 - $OUT <<'PY'
+import json, sys, glob
+for f in sorted(glob.glob(sys.argv[1] + "/bench*.log")):
+    ln = [l for l in open(f) if l.startswith("{")]
+    if not ln:
+        print(f, "no JSON"); continue
+    d = json.loads(ln[-1]); k = d["kernels"]
+    print(f.split("/")[-1], d["value"], "pairs/s", d["ms_per_step"], "ms/step frac", d["corrblock_frac"],
+          "gemm", k["build"]["ms_per_launch"], "pack", k.get("pack", {}).get("ms_per_launch"), "lookup", k["lookup"]["ms_per_launch"])
+PY
+bash tools/profile.sh $TAG/prof

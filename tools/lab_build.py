@@ -385,6 +385,8 @@ PATCHES["onecu16"] = [("build.hip", """__global__ __launch_bounds__(256, 2) void
     __shared__ __attribute__((aligned(16))) char smem[SLDS + (SQ + 256) * 4];""", """__global__ __launch_bounds__(256, 1) void build_split16_kernel(BuildParams P) {
     // ALL LDS in this one array (cdna_hip_programming.md trap 4(a), see build_split_kernel)
     __shared__ __attribute__((aligned(16))) char smem[SLDS + (SQ + 256) * 4 + 16384];""")]
+# (round 3: split16 level-0 lines stored straight from their lanes, no LDS transpose -- the source
+# option is gone: 4.8 ms and 5.4 GB written, profiles/r03_lab/r3h_*)
 # the tree as it is (the baseline of an A/B against an edited tree)
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
