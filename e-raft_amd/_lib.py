@@ -7,6 +7,7 @@ kernels run in torch's HIP context on torch's streams and caching-allocator poin
 There is no fallback: if libecorr.so is missing or was built for another target, every entry point
 raises.  Build it with `make -C e-raft_amd/csrc` or `python -c "import __graft_entry__ as g; g.build()"`.
 """
+import contextlib
 import ctypes
 import os
 
@@ -135,6 +136,15 @@ def layout(rows: int, H: int, W: int, levels: int):
 
 def stream_of(t: torch.Tensor):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+_same_device = contextlib.nullcontext()
+
+
+def on_device(dev: torch.device):
+    """torch.cuda.device(dev) only when dev is not already current: the launches then go to dev's
+    context, and the per-call host cost stays off the lookup path (12 calls per pair)."""
+    return _same_device if torch.cuda.current_device() == dev.index else torch.cuda.device(dev)
 
 
 # Which GEMM builds level 0 (include/ecorr.h): "split" = ecorr_build_split (f16 matrix cores on

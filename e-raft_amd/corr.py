@@ -71,7 +71,7 @@ class CorrBlock:
         self._device = fmap1.device
         Q = H * W
         self._h, self._w, self._off = _lib.layout(B * Q, H, W, num_levels)
-        with torch.cuda.device(self._device):
+        with _lib.on_device(self._device):
             self._pyramid = _lib.build_pyramid(fmap1, fmap2, B, D, H, W, Q, num_levels, self._off,
                                                "CorrBlock build")
         self._rows = B * Q
@@ -99,7 +99,7 @@ class CorrBlock:
         coords = coords.contiguous()   # the reference accepts any strides (permute + reshape)
         K = 2 * self.radius + 1
         C = self.num_levels * K * K
-        with torch.cuda.device(self._device):
+        with _lib.on_device(self._device):
             out = torch.empty((B, C, H, W), dtype=torch.float32, device=self._device)
             _lib.check(_lib.lib().ecorr_lookup(
                 self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, self.num_levels,
@@ -131,7 +131,7 @@ class CorrBlock:
             bias = bias.contiguous()
         wt = weight.reshape(O, C).contiguous()   # the conv weight [O, C, 1, 1] as is
         coords = coords.contiguous()
-        with torch.cuda.device(self._device):
+        with _lib.on_device(self._device):
             out = torch.empty((B, O, H, W), dtype=torch.float32, device=self._device)
             _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu(
                 self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, self.num_levels,

@@ -93,7 +93,7 @@ class RowExchange:
         recv = self.gather_chunks(B, C, W, torch.float32, device)
         _require_device_f32("rows exchange buffer", recv)
         out = torch.empty((B, C, self.H, W), dtype=torch.float32, device=recv.device)
-        with torch.cuda.device(recv.device):
+        with _lib.on_device(recv.device):
             _lib.check(_lib.lib().ecorr_rows_assemble(
                 recv.data_ptr(), self.chunk_elems(B, C, W), self.world, B, C, self.H, W, out.data_ptr(),
                 _lib.stream_of(out)), "RowExchange assemble")
@@ -176,7 +176,7 @@ class RowShardedCorrBlock:
         self._device = fmap2.device
         self.q_count = self.counts[self.rank] * W
         self._h, self._w, self._off = _lib.layout(B * self.q_count, H, W, num_levels)
-        with torch.cuda.device(self._device):
+        with _lib.on_device(self._device):
             self._pyramid = _lib.build_pyramid(fmap1_rows, fmap2, B, D, H, W, self.q_count, num_levels,
                                                self._off, "RowShardedCorrBlock build")
         self._levels_cache = None
@@ -205,7 +205,7 @@ class RowShardedCorrBlock:
 
     def _lookup_into(self, coords_rows, out):
         B, _, H, W = self._shape
-        with torch.cuda.device(self._device):
+        with _lib.on_device(self._device):
             _lib.check(_lib.lib().ecorr_lookup(
                 self._pyramid.data_ptr(), coords_rows.data_ptr(), B, H, W, self.q_count,
                 self.num_levels, self.radius, out.data_ptr(), _lib.stream_of(out)),
@@ -226,7 +226,7 @@ class RowShardedCorrBlock:
         if tuple(coords.shape) != (B, 2, H, W):
             raise RuntimeError(f"coords shape {tuple(coords.shape)} != {(B, 2, H, W)}")
         r0, rr = self.starts[self.rank], self.counts[self.rank]
-        return self._local_coords(coords[:, :, r0:r0 + rr])
+        return self._local_coords(coords if rr == H else coords[:, :, r0:r0 + rr])
 
     def __call__(self, coords):
         B, _, H, W = self._shape
@@ -264,7 +264,7 @@ class RowShardedCorrBlock:
             out = torch.empty((B, O, H, W), dtype=torch.float32, device=self._device)
         else:
             out = self._ex.send_slab(B, O, W, device=self._device)
-        with torch.cuda.device(self._device):
+        with _lib.on_device(self._device):
             _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu(
                 self._pyramid.data_ptr(), coords_rows.data_ptr(), B, H, W, self.q_count, self.num_levels,
                 self.radius, wt.data_ptr(), None if bias is None else bias.data_ptr(), O, out.data_ptr(),
