@@ -25,4 +25,5 @@ for f in sorted(glob.glob(sys.argv[1] + "/bench*.log")):
     print(f.split("/")[-1], d["value"], "pairs/s", d["ms_per_step"], "ms/step frac", d["corrblock_frac"],
           "gemm", k["build"]["ms_per_launch"], "pack", k.get("pack", {}).get("ms_per_launch"), "lookup", k["lookup"]["ms_per_launch"])
 PY
+[ -n "$NOPROF" ] && exit 0
 bash tools/profile.sh $TAG/prof
