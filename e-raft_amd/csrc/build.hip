@@ -755,7 +755,11 @@ static_assert(S16NB != 4 || S16COPIES != 4 || S16QL != 8 ||
 // vector issue half the time, so its VALU count is the cost: every address is 32-bit and hoisted
 // out of the query-group loop (the quadrant geometry is the lane's; only the query row changes),
 // and the cross-lane steps are v_permlane16/32_swap.
-template <bool MUL>
+// FULL (a whole 256-query tile whose first query row starts a 64-row group, as every tile of the
+// BASELINE configs does): every store's query-row term is wave-uniform, so it rides in the scalar
+// soffset and a lane's voffset is one constant per store kind (SOOB where its piece lies outside
+// the level) -- no per-store address VALU, compare or select.
+template <bool MUL, bool FULL>
 __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (&acc)[4][8], char* const xw, int qw,
                                                  const int* exq, const int* ext, const float* fst, const NTile& tc,
                                                  int b, int q0, int lane) {
@@ -826,6 +830,23 @@ __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (
     auto st2 = [&](__amdgpu_buffer_rsrc_t rs, int off, bool ok, floatx2 v) {
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, ok ? off : SOOB, 0, ST_L01);
     };
+    // FULL: lane-constant offsets (query-row term qn of the 16-query group, the lane's piece; FOOB
+    // where the piece lies outside the level) plus a wave-uniform term (qg, the store, the wave's
+    // 64-row group = its index: rl0 == 0) -- one v_add per store.  (The uniform term as the
+    // instruction's scalar soffset instead dropped ~0.03% of the level-0 stores at B = 16 on gfx950,
+    // round-3 tools/diag_full.py; added into the voffset every store lands.)
+    constexpr int FOOB = 0x70000000;   // + any uniform term stays beyond every slab, below 2^31
+    const int qwu = __builtin_amdgcn_readfirstlane(qw);   // wave-uniform (qw = 64 wave)
+    const int v0 = l0ok ? l0off - qw * l0stride : FOOB;   // + (qw + 16 qg + s) l0stride
+    const int v1x = b1x >= 0 ? (qn * 8 + b1x) * 4 : FOOB, v1y = b1y >= 0 ? (qn * 8 + b1y) * 4 : FOOB;
+    const int v2 = b2 >= 0 ? (qn * 8 + b2) * 4 : FOOB, v3 = b3 >= 0 ? (qn * 2 + b3) * 4 : FOOB;
+    const int grpw = qwu >> 6;   // FULL: the wave's interleaved group (block-relative)
+    auto fst4 = [&](__amdgpu_buffer_rsrc_t rs, int voff, int uoff, floatx4 v) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), rs, voff + uoff, 0, ST_L01);
+    };
+    auto fst2 = [&](__amdgpu_buffer_rsrc_t rs, int voff, int uoff, floatx2 v) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, voff + uoff, 0, ST_L01);
+    };
     // fast scale: every exponent of the wave's queries and of the panel's targets in [-63, 63]
     bool fast_scale;
     {
@@ -877,9 +898,11 @@ __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (
         for (int tg = 0; tg < 8; ++tg)
             *reinterpret_cast<floatx4*>(xr + lane * S16LS + 16 * tg) = floatx4{v[tg][0], v[tg][1], v[tg][2], v[tg][3]};
 #pragma unroll
-        for (int s = 0; s < 8; ++s)
-            st4(r0, l0off + (16 * qg + s) * l0stride, l0ok && l0q + 16 * qg + s < nq,
-                *reinterpret_cast<const floatx4*>(xr + (s + 8 * jl) * S16LS + 16 * pc));
+        for (int s = 0; s < 8; ++s) {
+            const floatx4 x = *reinterpret_cast<const floatx4*>(xr + (s + 8 * jl) * S16LS + 16 * pc);
+            if (FULL) fst4(r0, v0, (qwu + 16 * qg + s) * l0stride, x);
+            else st4(r0, l0off + (16 * qg + s) * l0stride, l0ok && l0q + 16 * qg + s < nq, x);
+        }
         if (L < 2) continue;
         // this lane's query row in its interleaved group
         const int rr = rl0 + ql + qn;
@@ -909,13 +932,19 @@ __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (
                 x[c] = __uint_as_float(sw[0]);
                 y[c] = __uint_as_float(sw[1]);
             }
-            const int base1 = grp * G1 + rin * 8;
-            st4(r1, (base1 + b1x) * 4, qok && b1x >= 0, floatx4{x[0], x[1], x[2], x[3]});
-            st4(r1, (base1 + b1y) * 4, qok && b1y >= 0, floatx4{y[0], y[1], y[2], y[3]});
+            if (FULL) {
+                fst4(r1, v1x, (grpw * G1 + 16 * qg * 8) * 4, floatx4{x[0], x[1], x[2], x[3]});
+                fst4(r1, v1y, (grpw * G1 + 16 * qg * 8) * 4, floatx4{y[0], y[1], y[2], y[3]});
+            } else {
+                const int base1 = grp * G1 + rin * 8;
+                st4(r1, (base1 + b1x) * 4, qok && b1x >= 0, floatx4{x[0], x[1], x[2], x[3]});
+                st4(r1, (base1 + b1y) * 4, qok && b1y >= 0, floatx4{y[0], y[1], y[2], y[3]});
+            }
         }
         if (L < 3) continue;
         // level 2: 4 lanes x 8 B = one query's 2 x 4 block (band: half of two)
-        st2(r2, (grp * G2 + rin * 8 + b2) * 4, qok && b2 >= 0, floatx2{l2[0], l2[1]});
+        if (FULL) fst2(r2, v2, (grpw * G2 + 16 * qg * 8) * 4, floatx2{l2[0], l2[1]});
+        else st2(r2, (grp * G2 + rin * 8 + b2) * 4, qok && b2 >= 0, floatx2{l2[0], l2[1]});
         if (L < 4 || tc.band) continue;
         // level 3 (regular tiles): pixel kb >> 1 of the tile's 1 x 2 from the 2 x 2 level-2 pixels of
         // lanes kb (row 0, kb even) and kb + 1 (row 1), brought over by a row swap; lane kb = 0 takes
@@ -924,7 +953,8 @@ __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (
         const auto o1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l2[1]), __float_as_uint(l2[1]), false, false);
         const float p3 = pool4(l2[0], l2[1], __uint_as_float(o0[1]), __uint_as_float(o1[1]));
         const auto p3s = __builtin_amdgcn_permlane32_swap(__float_as_uint(p3), __float_as_uint(p3), false, false);
-        st2(r3, (grp * G3 + rin * 2 + b3) * 4, qok && b3 >= 0, floatx2{p3, __uint_as_float(p3s[1])});
+        if (FULL) fst2(r3, v3, (grpw * G3 + 16 * qg * 2) * 4, floatx2{p3, __uint_as_float(p3s[1])});
+        else st2(r3, (grp * G3 + rin * 2 + b3) * 4, qok && b3 >= 0, floatx2{p3, __uint_as_float(p3s[1])});
     }
 }
 
@@ -1002,20 +1032,24 @@ __global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
         a.h = *reinterpret_cast<const halfx8*>(p);
         a.l = *reinterpret_cast<const halfx8*>(p + 1024);
     };
-    // per element and pair: hi*hi, lo*hi, hi*lo (4 independent accumulators between dependent
-    // MFMAs).  Inline asm with the accumulator constrained to VGPRs at every MFMA (gfx950's
-    // register file is unified: 128 accumulator VGPRs + the loop's ~100 fit the 256 of two waves
-    // per SIMD, and the epilogue's VALU then reads them without 128 v_accvgpr_read per wave); with
+    // per element and pair: hi*hi, lo*hi, hi*lo.  Inline asm with the accumulator constrained to
+    // VGPRs at every MFMA (gfx950's register file is unified: 128 accumulator VGPRs + the loop's
+    // ~100 fit the 256 of two waves per SIMD, and the epilogue's VALU then reads them without 128
+    // v_accvgpr_read per wave); with
     // the builtin, hipcc renames accumulator tiles between AGPRs and VGPRs inside the loop
     // (v_accvgpr copies, 48 spilled VGPRs).  Its waitcnt pass still covers the fragment operands.
     auto mfma = [&](floatx4& c, const halfx8& a, const halfx8& bq) {
         asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(bq));
     };
+    // order: hi*hi and lo*hi per group (the query fragment stays the B operand of two MFMAs in a
+    // row), then hi*lo -- round-3 A/B 597.7 vs 605.9 us for hh x4, lh x4, hl x4 (same instructions;
+    // fewer operand changes between consecutive MFMAs is the suspected, unmeasured, mechanism)
     auto mfma_tg = [&](const AF& a, const QF& q, int tg) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) mfma(acc[g][tg], a.h, q.h[g]);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) mfma(acc[g][tg], a.l, q.h[g]);
+        for (int g = 0; g < 4; ++g) {
+            mfma(acc[g][tg], a.h, q.h[g]);
+            mfma(acc[g][tg], a.l, q.h[g]);
+        }
 #pragma unroll
         for (int g = 0; g < 4; ++g) mfma(acc[g][tg], a.h, q.l[g]);
     };
@@ -1071,7 +1105,11 @@ __global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
     for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int t = 0; t < 8; ++t) asm volatile("" : "+v"(acc[g][t]));
-    split16_epilogue<MUL>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+    // FULL: a whole query tile starting a 64-row group (block-uniform)
+    if (q0 + SQ <= P.q_count && (((int64_t)b * P.q_count + q0) & (kGroup - 1)) == 0)
+        split16_epilogue<MUL, true>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+    else
+        split16_epilogue<MUL, false>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
 }
 
 // ============================================================================================

@@ -27,17 +27,21 @@ namespace ecorr {
 // origin column in both modes: phase 2's offset of sample a from the origin is a (+ a floor flip)
 // for every query, and lanes = queries at the odd stride SP hit distinct banks.  (Unshifted, the
 // even rounding made the offsets a or a + 1 at random across lanes: 49% of the LDS cycles were
-// bank conflicts.)  A staged row holds S + 1 slots in PAIR mode: slot S takes the shifted-out
-// column of odd origins (never read), slot -1 of row 0 the first one (W0 = 1 leading slot).
+// bank conflicts.)  The half of a pair that falls outside the S-slot row (the shifted-out column
+// of an odd origin, or column S of an even one; never read) goes to the dummy slot at the end of win[],
+// so rows hold S slots: 31.7 KB at r = 4, five workgroups per CU (S + 1 slots: 34.8 KB, four;
+// round 3 A/B 41.7 / 45.4 / 41.3 vs 41.9 / 45.8 / 42.8 us on the smooth / sigma-3 / sigma-40 fields).
 template <int R, int QB, bool PAIR = false>
 struct WindowBuf {
     static constexpr int K = 2 * R + 1;   // samples per axis
     static constexpr int KK = K * K;
     static constexpr int S = 2 * R + 3;   // staged window side (rows)
-    static constexpr int SW = PAIR ? S + 1 : S;   // staged row length
-    static constexpr int SP = (S * SW) | 1;       // odd per-query stride: conflict-free lanes = queries
-    static constexpr int W0 = PAIR ? 1 : 0;       // query g's window starts at win[W0 + g SP]
-    float win[W0 + QB * SP];
+    static constexpr int SW = S;          // staged row length
+    static constexpr int SP = (S * SW) | 1;   // odd per-query stride: conflict-free lanes = queries
+    static constexpr int W0 = PAIR ? 1 : 0;   // query g's window starts at win[W0 + g SP] (PAIR: the
+                                              // first item's base W0 - 1 stays >= 0, "no item" < 0)
+    static constexpr int DUMMY = W0 + QB * SP;   // the never-read slot of out-of-row pair halves
+    float win[W0 + QB * SP + 1];
     // per query: window origin x, y and (mode | needed cols << 8 | needed rows << 16), where mode
     // 0 = staged, 1 = direct gather (coordinates that do not fit the window), 2 = past the range.
     int org[QB][3];
@@ -124,12 +128,55 @@ __device__ __forceinline__ void stage_level(WindowStage<R, QB, PAIR>& st, const 
     stage_windows<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid);
 }
 
+// Phase 1's loads in flight: this thread's work items (window columns or column pairs, each S rows)
+// and their LDS destinations (-1: no item).
+template <int R, int QB, int NTQ, bool PAIR>
+struct StageRegs {
+    static constexpr int S = 2 * R + 3, V = PAIR ? 2 : 1;
+    static constexpr int NPX = (WindowBuf<R, QB, PAIR>::SW + V - 1) / V;   // work items per query
+    static constexpr int ITEMS = QB * NPX;
+    static constexpr int NCOL = (ITEMS + NTQ - 1) / NTQ;
+    float vals[NCOL][S][V];
+    int dst[NCOL];
+    int skip[NCOL];   // PAIR: the half (0 or 1) of the item that lies outside the row, else -1
+};
+
+// Phase 1, first half: issue this thread's window loads for level lv of queries [q0, q0 + QB) of
+// batch item b (origins from st.org) into registers; stage_commit() writes them to st.win.
+template <int R, int QB, int NTQ, bool PAIR>
+__device__ __forceinline__ void stage_issue(const WindowBuf<R, QB, PAIR>& st, const LookupParams& P, int lv, int b,
+                                            int q0, int tid, StageRegs<R, QB, NTQ, PAIR>& sr);
+
+// Phase 1, second half: the staged values into the LDS windows (no barrier).
+template <int R, int QB, int NTQ, bool PAIR>
+__device__ __forceinline__ void stage_commit(WindowBuf<R, QB, PAIR>& st, const StageRegs<R, QB, NTQ, PAIR>& sr) {
+    using SR = StageRegs<R, QB, NTQ, PAIR>;
+    constexpr int SW = WindowBuf<R, QB, PAIR>::SW, DUMMY = WindowBuf<R, QB, PAIR>::DUMMY;
+#pragma unroll
+    for (int c = 0; c < SR::NCOL; ++c)
+        if (sr.dst[c] >= 0)
+#pragma unroll
+            for (int ry = 0; ry < SR::S; ++ry)
+#pragma unroll
+                for (int v = 0; v < SR::V; ++v)
+                    st.win[sr.skip[c] == v ? DUMMY : sr.dst[c] + ry * SW + v] = sr.vals[c][ry][v];
+}
+
 // Phase 1 for level lv of queries [q0, q0 + QB) of batch item b, from st.org; ends with a barrier.
 template <int R, int QB, int NTQ, bool PAIR>
 __device__ __forceinline__ void stage_windows(WindowBuf<R, QB, PAIR>& st, const LookupParams& P, int lv, int b,
                                               int q0, int tid) {
+    StageRegs<R, QB, NTQ, PAIR> sr;
+    stage_issue<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid, sr);
+    stage_commit<R, QB, NTQ, PAIR>(st, sr);
+    __syncthreads();
+}
+
+template <int R, int QB, int NTQ, bool PAIR>
+__device__ __forceinline__ void stage_issue(const WindowBuf<R, QB, PAIR>& st, const LookupParams& P, int lv, int b,
+                                            int q0, int tid, StageRegs<R, QB, NTQ, PAIR>& sr) {
     using WS = WindowBuf<R, QB, PAIR>;
-    constexpr int S = WS::S, SW = WS::SW, SP = WS::SP;
+    constexpr int S = WS::S, SP = WS::SP;
     constexpr int V = PAIR ? 2 : 1;   // window columns per work item (PAIR: one 8-byte load)
     const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
     const int64_t hw = P.lsz[lv];  // floats per query image
@@ -147,9 +194,8 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB, PAIR>& st, const 
     // over this group's slab of the level: an element outside the image gets an out-of-range
     // offset and the hardware range check returns 0 -- zero padding with no branch and no select,
     // so all NCOL*S loads of a thread issue back to back.
-    constexpr int NPX = SW / V;   // work items per query
-    constexpr int ITEMS = QB * NPX;
-    constexpr int NCOL = (ITEMS + NTQ - 1) / NTQ;
+    using SR = StageRegs<R, QB, NTQ, PAIR>;
+    constexpr int NPX = SR::NPX, ITEMS = SR::ITEMS, NCOL = SR::NCOL;
     const int nq = min(QB, P.q_count - q0);
     const int64_t span = ntx < 0 ? (((R0 + nq - 1) >> 6) - g0 + 1) * kGroup * hw : nq * hw;
     const __amdgpu_buffer_rsrc_t rsrc =
@@ -162,8 +208,8 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB, PAIR>& st, const 
     const int step_in = 4 << sx;
     const int step_wrap = tiled ? 128 * ntx - 96 : ilv ? 4 * (-ntx * kGroup * (1 << (sy + sx)) - ymask * (1 << sx)) : 4 * w;
     constexpr int OOB = 0x7ffffff0;   // beyond any slab: reads as 0
-    float vals[NCOL][S][V];
-    int dst[NCOL];
+    auto& vals = sr.vals;
+    auto& dst = sr.dst;
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) {
         const int it = tid + c * NTQ;
@@ -177,6 +223,7 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB, PAIR>& st, const 
         // only the needed corner rectangle touches memory; the slack row/column reads 0 for free
         const bool colin = live && (info & 0xff) == 0 && rx < ((info >> 8) & 0xff) + odd && (unsigned)x < (unsigned)w;
         dst[c] = live ? WS::W0 + gq * SP + rx - odd : -1;
+        sr.skip[c] = PAIR && odd && rx == 0 ? 0 : PAIR && !odd && rx == S - 1 ? 1 : -1;
         // rows ry in [rlo, rhi) are needed and inside the image; the column's byte offset walks
         // down the rows incrementally (tiled: +8 floats inside a tile, + one tile row minus 24 from
         // in-tile row 3; interleaved likewise per block; compact: +w) instead of re-deriving the
@@ -208,14 +255,6 @@ __device__ __forceinline__ void stage_windows(WindowBuf<R, QB, PAIR>& st, const 
             ym = (ym + 1) & ymask;
         }
     }
-#pragma unroll
-    for (int c = 0; c < NCOL; ++c)
-        if (dst[c] >= 0)
-#pragma unroll
-            for (int ry = 0; ry < S; ++ry)
-#pragma unroll
-                for (int v = 0; v < V; ++v) st.win[dst[c] + ry * SW + v] = vals[c][ry][v];
-    __syncthreads();
 }
 
 // Exact direct gather of one sample of query p (slab index) from its floors and weights, for
