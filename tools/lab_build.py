@@ -315,8 +315,8 @@ PATCHES["st16"] = [
     ("build.hip", """    __syncthreads();      // ... in every wave: the panel buffers are the epilogue's scratch""",
      """    __syncthreads();      // ... in every wave: the panel buffers are the epilogue's scratch
     const unsigned long long c_loop1 = __builtin_amdgcn_s_memtime(), r_loop1 = __builtin_amdgcn_s_memrealtime();"""),
-    ("build.hip", """    split16_epilogue<MUL>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
-}""", """    split16_epilogue<MUL>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+    ("build.hip", """        split16_epilogue<MUL, false>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+}""", """        split16_epilogue<MUL, false>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
     __syncthreads();
     if (tid == 0 && blockIdx.x < 65536) {
         unsigned long long* g = g_st16[blockIdx.x];
@@ -387,6 +387,39 @@ PATCHES["onecu16"] = [("build.hip", """__global__ __launch_bounds__(256, 2) void
     __shared__ __attribute__((aligned(16))) char smem[SLDS + (SQ + 256) * 4 + 16384];""")]
 # (round 3: split16 level-0 lines stored straight from their lanes, no LDS transpose -- the source
 # option is gone: 4.8 ms and 5.4 GB written, profiles/r03_lab/r3h_*)
+# the query-stationary persistent build (build_qs_kernel) in place of build_split16_kernel
+PATCHES["qs"] = [("build.hip", "constexpr bool kBuildQS = false;", "constexpr bool kBuildQS = true;")]
+# QS with the two half-panel LDS buffers swapped (does LDS-DMA reach beyond 64 KB?)
+# QS debug: the previous half's epilogue after this half's MFMAs instead of interleaved
+PATCHES["qsseq"] = PATCHES["qs"] + [
+    ("build.hip", """            if constexpr (EPI) epi_step(AE, kc);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+""", """            __builtin_amdgcn_sched_barrier(0);
+        });
+        if constexpr (EPI) {
+            asm volatile("s_nop 15");
+            asm volatile("s_nop 15");
+            qs_static_for<NCP * 16>([&](auto kc) QS_INLINE {
+                epi_step(AE, kc);
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        }
+""")]
+# QS timing probes (wrong results): MFMAs and panel transfers only / epilogue and transfers only
+PATCHES["qsnoepi"] = PATCHES["qs"] + [
+    ("build.hip", "            if constexpr (EPI) epi_step(AE, kc);\n", ""),
+    ("build.hip", "        if constexpr (EPI) flush();\n", ""),
+]
+PATCHES["qsnomf"] = PATCHES["qs"] + [
+    ("build.hip", '''        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));''',
+     '''        asm volatile("" : "+v"(c) : "v"(a), "a"(b));'''),
+    ("build.hip", '''        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "a"(b));''',
+     '''        asm volatile("v_mov_b32 %0, 0" : "=v"(c[0]) : "v"(a), "a"(b));'''),
+]
+# QS epilogue stores with the default cache policy (write-back L2) instead of nt | sc1
+PATCHES["qsst0"] = PATCHES["qs"] + [("build.hip", "constexpr int QS_ST = 18;", "constexpr int QS_ST = 0;")]
+PATCHES["qsnomfst0"] = PATCHES["qsnomf"] + PATCHES["qsst0"][1:]
 # the tree as it is (the baseline of an A/B against an edited tree)
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
