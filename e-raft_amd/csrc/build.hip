@@ -1198,8 +1198,14 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int qn = lane & 15, kb = lane >> 4;
-    const int ub = (int)((int64_t)blockIdx.x * units / gridDim.x);
-    const int ue = (int)((int64_t)(blockIdx.x + 1) * units / gridDim.x);
+    // the block's unit sequence s = 0 .. ue - 1: R full rounds in lockstep -- round r is query tile
+    // r G + block, n-tiles 0 .. n_nt - 1 in order, so at any time every block reads the same n-tile
+    // panel of its batch (L2 / MALL hits; with each block on its own n-tile phase the panels came
+    // from HBM again per query tile: 1.6 GB) -- then an even contiguous share of the rest
+    const int G = gridDim.x, NQT = units / P.n_nt, R = NQT / G;
+    const int Ur = (NQT - R * G) * P.n_nt;
+    const int rb = (int)((int64_t)blockIdx.x * Ur / G), re = (int)((int64_t)(blockIdx.x + 1) * Ur / G);
+    const int ub = 0, ue = R * P.n_nt + re - rb;
     if (ub >= ue) return;   // block-uniform
     char* const stg = smem + 2 * QS_HALF + wave * QS_STG;                          // [64][8] L2, then [64][2] L3
     float* const xf = reinterpret_cast<float*>(smem + 2 * QS_HALF + 4 * QS_STG);   // [3][64] 2^-e_t (clamped)
@@ -1210,10 +1216,12 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
     const int nbx1 = -P.lntx[1], nbx2 = -P.lntx[2], nbx3 = -P.lntx[3];
 
     struct Unit { int b, qt, nt; };
-    auto decode = [&](int u) QS_INLINE {
+    auto decode = [&](int s) QS_INLINE {
         Unit t;
-        t.nt = u % P.n_nt;
-        const int r = u / P.n_nt;
+        const int lin = s < R * P.n_nt ? (s / P.n_nt * G + (int)blockIdx.x) * P.n_nt + s % P.n_nt
+                                       : R * G * P.n_nt + rb + (s - R * P.n_nt);
+        t.nt = lin % P.n_nt;
+        const int r = lin / P.n_nt;
         t.qt = r % P.n_qt;
         t.b = r / P.n_qt;
         return t;

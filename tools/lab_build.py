@@ -420,6 +420,17 @@ PATCHES["qsnomf"] = PATCHES["qs"] + [
 # QS epilogue stores with the default cache policy (write-back L2) instead of nt | sc1
 PATCHES["qsst0"] = PATCHES["qs"] + [("build.hip", "constexpr int QS_ST = 18;", "constexpr int QS_ST = 0;")]
 PATCHES["qsnomfst0"] = PATCHES["qsnomf"] + PATCHES["qsst0"][1:]
+# QS timing probes: no wait for the panel past the first unit (races: timing only); the previous
+# half's whole epilogue before this half's MFMAs (its stores get the whole half to complete)
+PATCHES["qsnowait"] = PATCHES["qs"] + [("build.hip", "    using WN = std::integral_constant<int, QS_NST>;",
+                                        "    using WN = std::integral_constant<int, 63>;")]
+PATCHES["qspre"] = PATCHES["qs"] + [
+    ("build.hip", "        if constexpr (EPI) epi_begin();\n        AF af[2];",
+     "        if constexpr (EPI) {\n            epi_begin();\n            qs_static_for<NCP * 16>([&](auto kc) QS_INLINE {\n"
+     "                epi_step(AE, kc);\n                __builtin_amdgcn_sched_barrier(0);\n            });\n            flush();\n        }\n        AF af[2];"),
+    ("build.hip", "            if constexpr (EPI) epi_step(AE, kc);\n", ""),
+    ("build.hip", "        if constexpr (EPI) flush();\n", ""),
+]
 # the tree as it is (the baseline of an A/B against an edited tree)
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs

@@ -100,8 +100,10 @@ int main(int argc, char** argv) {
         for (int nb : {32, 64, 128, 256, 512, 1024, 2048}) {
             g_blocks = nb;
             const float a = run<1, 18>(b2, reps), c = run<1, 0>(b2, reps), d = run<0, 18>(b2, reps);
-            printf("blocks %5d: oct128 nt|sc1 %7.0f GB/s  plain %7.0f  coal nt|sc1 %7.0f\n", nb, mv / (a * 1e-3) / 1e9,
-                   mv / (c * 1e-3) / 1e9, mv / (d * 1e-3) / 1e9);
+            const float e = run<2, 18>(b2, reps), f = run<2, 0>(b2, reps);
+            printf("blocks %5d: oct128 nt|sc1 %7.0f GB/s  plain %7.0f  coal nt|sc1 %7.0f  quad64 nt|sc1 %7.0f  plain %7.0f\n", nb,
+                   mv / (a * 1e-3) / 1e9, mv / (c * 1e-3) / 1e9, mv / (d * 1e-3) / 1e9, mv / (e * 1e-3) / 1e9,
+                   mv / (f * 1e-3) / 1e9);
         }
         return 0;
     }
