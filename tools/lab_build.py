@@ -431,6 +431,8 @@ PATCHES["qspre"] = PATCHES["qs"] + [
     ("build.hip", "            if constexpr (EPI) epi_step(AE, kc);\n", ""),
     ("build.hip", "        if constexpr (EPI) flush();\n", ""),
 ]
+# split16 level-0/1 stores as nt | sc1 instead of nt
+PATCHES["st18"] = [("build.hip", "constexpr int ST_L01 = 2; ", "constexpr int ST_L01 = 18;")]
 # the tree as it is (the baseline of an A/B against an edited tree)
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
