@@ -1369,7 +1369,20 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
     float cd[2];       // the partner row's two values of the current level-1 pixel
     float l2v[2];      // level-2 pixels (lanes kb < 2) per line
     float sw1x[2], sw1y[2];   // the level-1 store swap per line (kept for level 2)
+    // store addressing of the half being finished (rows0 % 64 == 0, launch_build's condition):
+    // offset = a lane constant (its query row qn of the 16-query group, its piece kb) + a
+    // wave-uniform term (query group, line / block, the wave's 64-row group) -- one v_add per store
+    __amdgpu_buffer_rsrc_t er0, er1;
+    int eu0[4], eu1[2];
+    const int l0lane = qn * l0stride + 16 * kb, l1lane = (qn * 8 + 2 * kb) * 4;
     auto epi_begin = [&]() QS_INLINE {
+        er0 = lvl_rsrc(0);
+        er1 = lvl_rsrc(1);
+        const int G1 = kGroup * (int)P.lsz[1] * 4;
+#pragma unroll
+        for (int tg = 0; tg < 4; ++tg) eu0[tg] = __builtin_amdgcn_readfirstlane(l0_line(tg) + 64 * wave * l0stride);
+#pragma unroll
+        for (int ln = 0; ln < 2; ++ln) eu1[ln] = __builtin_amdgcn_readfirstlane(l1_block(ln) + wave * G1);
         const float* s = C.qfast ? xf + C.slot * 64 : reinterpret_cast<const float*>(xe + C.slot * 64);
 #pragma unroll
         for (int tg = 0; tg < 4; ++tg) st[tg] = *reinterpret_cast<const floatx4*>(s + 16 * tg + 4 * kb);
@@ -1394,14 +1407,14 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
     // g (32 steps): per target group tg five steps -- scale two values, two values, the level-0
     // half-line store, the level-1 pixel (two steps) -- then the two level-1 line stores, the two
     // level-2 pixels (two steps each), the level-3 pixel
-    auto epi_step = [&](floatx4 (&A)[4][4], auto kc) QS_INLINE {
+    auto epi_step = [&](floatx4 (&A)[4][4], auto kc, auto fast_c) QS_INLINE {
         constexpr int k = decltype(kc)::value;
+        constexpr bool FAST = decltype(fast_c)::value;
         constexpr int g = k >> 5, m = k & 31;
-        const int qlw = 64 * wave + 16 * g + qn;   // the lane's query, wave-local row of the tile
         if constexpr (m < 20) {
             constexpr int tg = m / 5, ms = m % 5;
             if constexpr (ms < 2) {   // scale values 2 ms, 2 ms + 1
-                if (tfast) {
+                if constexpr (FAST) {
                     const floatx2 f = floatx2{C.sq[g], C.sq[g]} * floatx2{st[tg][2 * ms], st[tg][2 * ms + 1]};
                     const floatx2 x = floatx2{A[g][tg][2 * ms], A[g][tg][2 * ms + 1]} * f;
                     v[2 * ms] = x[0];
@@ -1412,8 +1425,8 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
                     v[2 * ms + 1] = ldexpf(A[g][tg][2 * ms + 1], n + __float_as_int(st[tg][2 * ms + 1]));
                 }
             } else if constexpr (ms == 2) {   // level-0 half line (range-checked per query image by the descriptor)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), lvl_rsrc(0),
-                                                       qlw * l0stride + 16 * kb + l0_line(tg), 0, QS_ST);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), er0,
+                                                       l0lane + (eu0[tg] + 16 * g * l0stride), 0, QS_ST);
             } else if constexpr (ms == 3) {
                 // lanes < 32 (level-0 row 0 of the half line): a, b = own v0, v1, c, d = row 1's v0, v1;
                 // lanes >= 32: a, b = row 0's v2, v3, c, d = own v2, v3
@@ -1430,8 +1443,8 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
             const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(p1[2 * ln]), __float_as_uint(p1[2 * ln + 1]), false, false);
             sw1x[ln] = __uint_as_float(s[0]);
             sw1y[ln] = __uint_as_float(s[1]);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, floatx2{sw1x[ln], sw1y[ln]}), lvl_rsrc(1),
-                                                  ilv_row(1, qlw, 2 * kb) + l1_block(ln), 0, QS_ST);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, floatx2{sw1x[ln], sw1y[ln]}), er1,
+                                                  l1lane + (eu1[ln] + 16 * g * 8 * 4), 0, QS_ST);
         } else if constexpr (m < 26) {   // level-2 pixel of line (m - 22) >> 1 on lanes kb < 2 (two steps)
             constexpr int ln = (m - 22) >> 1;
             if constexpr (((m - 22) & 1) == 0) {
@@ -1491,7 +1504,9 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
     // ---- one half: wait for its panel, publish its exponents, start the next half's transfer, then
     // its MFMAs (buffer / accumulators PAR) interleaved with the previous half's epilogue
     int hs = 0;   // halves begun by this block (the exponent slot is hs % 3)
-    auto run_half = [&](auto par_c, auto mf_c, auto epi_c, auto wait_c, int u, int h) QS_INLINE {
+    // FAST: the half being finished takes the power-of-two scaling path (tfast, decided by epi_begin
+    // before the call: one branch per half, not one per scaling step)
+    auto run_half = [&](auto par_c, auto mf_c, auto epi_c, auto wait_c, auto fast_c, int u, int h) QS_INLINE {
         constexpr int PAR = decltype(par_c)::value;
         constexpr bool MF = decltype(mf_c)::value, EPI = decltype(epi_c)::value;
         constexpr int WAITN = decltype(wait_c)::value;
@@ -1508,7 +1523,6 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
             const int un = h == 0 ? u : u + 1, hn = h ^ 1;
             if (un < ue) issue_half(un, hn, PAR ^ 1);
         }
-        if constexpr (EPI) epi_begin();
         AF af[2];
         if constexpr (MF) read_a(PAR, 0, 0, af[0]);
         qs_static_for<NCP * 16>([&](auto kc) QS_INLINE {
@@ -1532,7 +1546,7 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
                     else mfma(AM[g][tg], av, bv);
                 });
             }
-            if constexpr (EPI) epi_step(AE, kc);
+            if constexpr (EPI) epi_step(AE, kc, fast_c);
             __builtin_amdgcn_sched_barrier(0);
         });
         if constexpr (EPI) flush();
@@ -1555,8 +1569,14 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
     load_queries(cur);
     issue_half(ub, 0, 0);
     pin_queries();
-    run_half(I0(), BT(), BF(), W0(), ub, 0);
-    run_half(I1(), BT(), BT(), W0(), ub, 1);
+    // a half with an epilogue: its scaling path chosen once
+    auto run_epi = [&](auto par_c, auto mf_c, auto wait_c, int u, int h) QS_INLINE {
+        epi_begin();
+        if (tfast) run_half(par_c, mf_c, BT(), wait_c, BT(), u, h);
+        else run_half(par_c, mf_c, BT(), wait_c, BF(), u, h);
+    };
+    run_half(I0(), BT(), BF(), W0(), BT(), ub, 0);
+    run_epi(I1(), BT(), W0(), ub, 1);
     for (int u = ub + 1; u < ue; ++u) {
         const Unit t = decode(u);
         if (t.b != cur.b || t.qt != cur.qt) {   // a new query tile: drain, then reload (rare)
@@ -1565,10 +1585,10 @@ __global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int uni
             load_queries(cur);
             pin_queries();
         }
-        run_half(I0(), BT(), BT(), WN(), u, 0);
-        run_half(I1(), BT(), BT(), WN(), u, 1);
+        run_epi(I0(), BT(), WN(), u, 0);
+        run_epi(I1(), BT(), WN(), u, 1);
     }
-    run_half(I0(), BF(), BT(), W0(), ue, 0);   // the last half's epilogue alone
+    run_epi(I0(), BF(), W0(), ue, 0);   // the last half's epilogue alone
 }
 
 // ============================================================================================
@@ -2400,7 +2420,7 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
         // level 0 is always tiled and levels 1-3 interleaved, and absent levels have empty buffer
         // ranges); other D: build_split_kernel
         const bool s16 = (P.D + 15) / 16 == 2 * NCP;
-        const bool qs = kBuildQS && s16 && P.scale_is_mul;
+        const bool qs = kBuildQS && s16 && P.scale_is_mul && P.q_count % kGroup == 0;
         if (stages & 1) {
             if (qs) hipLaunchKernelGGL((pack_both_kernel<true, true>), dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
             else if (s16) hipLaunchKernelGGL((pack_both_kernel<true>), dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
