@@ -160,7 +160,8 @@ constexpr int QLOADS = 4;                   // query fragment loads per wave per
 constexpr int SLDS = 4 * 4 * 32 * 144;      // LDS bytes: the epilogue's transpose regions (> the K loop's)
 constexpr int SOOB = 0x7ffffff0;            // buffer offset beyond any panel: loads 0, touches nothing
 constexpr int ST_L01 = 2;                   // level-0/1 store cache policy: nt (A/B: 725 vs 731 us for nt sc1;
-                                            // plain and sc1 alone ~1000 us: the lines stay in L2 and evict the panels)
+                                            // plain and sc1 alone ~1000 us: the lines stay in L2 and evict the panels;
+                                            // split16, round 3: nt 605 vs nt sc1 627 us)
 constexpr int XS = 144;                     // LDS bytes per query of the epilogue's line transpose
 static_assert(4 * 4 * 32 * XS <= SLDS && SNBUF * SCHUNK <= SLDS, "LDS regions");
 
