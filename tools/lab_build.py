@@ -433,6 +433,18 @@ PATCHES["qspre"] = PATCHES["qs"] + [
 ]
 # split16 level-0/1 stores as nt | sc1 instead of nt
 PATCHES["st18"] = [("build.hip", "constexpr int ST_L01 = 2; ", "constexpr int ST_L01 = 18;")]
+# QS scheduling freedom: no scheduling barrier between the interleaved steps / one per two steps
+PATCHES["qsnosb"] = PATCHES["qs"] + [("build.hip", "            if constexpr (EPI) epi_step(AE, kc, fast_c);\n            __builtin_amdgcn_sched_barrier(0);",
+                                      "            if constexpr (EPI) epi_step(AE, kc, fast_c);")]
+PATCHES["qssb2"] = PATCHES["qs"] + [("build.hip", "            if constexpr (EPI) epi_step(AE, kc, fast_c);\n            __builtin_amdgcn_sched_barrier(0);",
+                                     "            if constexpr (EPI) epi_step(AE, kc, fast_c);\n            if constexpr ((decltype(kc)::value & 1) == 1) __builtin_amdgcn_sched_barrier(0);")]
+# QS timing probe: every pyramid store out of range (same instructions, no store traffic)
+PATCHES["qsnost"] = PATCHES["qs"] + [
+    ("build.hip", "P.lvl[0] + (int64_t)C.rows0 * P.lsz[0], 0, C.nq * l0stride, 0x00020000);",
+     "P.lvl[0] + (int64_t)C.rows0 * P.lsz[0], 0, 0, 0x00020000);"),
+    ("build.hip", "return __builtin_amdgcn_make_buffer_rsrc(P.lvl[L] + (int64_t)g0 * G, 0, gspan * G * 4, 0x00020000);",
+     "return __builtin_amdgcn_make_buffer_rsrc(P.lvl[L] + (int64_t)g0 * G, 0, 0 * gspan, 0x00020000);"),
+]
 # the tree as it is (the baseline of an A/B against an edited tree)
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
