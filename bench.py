@@ -485,11 +485,12 @@ def main():
 
     # every event record in the stream leaves a ~5 us gap between kernels (rocprof trace,
     # profiles/r02_final7): with the split build in batch mode its own stage events (before the
-    # operand pass, between the two launches, after the GEMM) bracket the build, so a step adds
-    # only the event after its lookups
+    # operand pass, between the two launches, after the GEMM) bracket the build, and a step's
+    # lookups end where the next step's operand pass begins, so only the last step records an
+    # event after its lookups
     lean = a.mode == "batch" and eraft_amd._lib.build_mode() == "split"
 
-    def step(ev=None):
+    def step(ev=None, last=True):
         if ev is not None and not lean:
             ev[0].record(stream)
         blk = make_block()
@@ -497,7 +498,7 @@ def main():
             ev[1].record(stream)
         for c in coords:
             blk(c)
-        if ev is not None:
+        if ev is not None and (last or not lean):
             ev[2].record(stream)
         return blk
 
@@ -512,7 +513,7 @@ def main():
         eraft_amd._lib.stage_events = stages = []   # split build: events around its two launches
         t0 = time.perf_counter()
         for k in range(a.steps):
-            step(evs[k])
+            step(evs[k], last=k == a.steps - 1)
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()
@@ -524,7 +525,10 @@ def main():
         if len(stages) != a.steps:
             raise RuntimeError(f"{len(stages)} split builds recorded for {a.steps} timed steps")
         build_ms = sum(st[0].elapsed_time(st[2]) for st in stages) / a.steps
-        look_ms = sum(st[2].elapsed_time(e[2]) for st, e in zip(stages, evs)) / a.steps / iters
+        # step k's lookups: from its GEMM's end to step k + 1's operand pass (the last step: to its
+        # own closing event)
+        ends = [stages[k + 1][0] for k in range(a.steps - 1)] + [evs[-1][2]]
+        look_ms = sum(st[2].elapsed_time(e) for st, e in zip(stages, ends)) / a.steps / iters
     else:
         build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps
         look_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps / iters
