@@ -46,6 +46,43 @@ SPLIT_MFMA_PER_PRODUCT = 3      # split build: lo*hi + hi*lo + hi*hi on the f16 
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak, spec
 
 
+class TimingEvent:
+    """A HIP timing event without the system-scope fence (hipEventDisableSystemFence): recording
+    it does not write back and invalidate the caches between two kernels, which a default event
+    (torch.cuda.Event) does -- about 5 us of idle GPU per record inside the timed region (rocprof
+    trace, profiles/r03_final3). Timing only; the timed region is still closed by a synchronize.
+    Calls the HIP runtime torch has loaded (one runtime per process: libamdhip64.so.7 by soname)."""
+    _hip = None
+    DISABLE_SYSTEM_FENCE = 0x20000000
+
+    def __init__(self):
+        import ctypes
+        if TimingEvent._hip is None:
+            TimingEvent._hip = ctypes.CDLL("libamdhip64.so.7")
+        self._ct = ctypes
+        self.h = ctypes.c_void_p()
+        rc = TimingEvent._hip.hipEventCreateWithFlags(ctypes.byref(self.h), ctypes.c_uint(self.DISABLE_SYSTEM_FENCE))
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags failed: {rc}")
+
+    def record(self, stream=None):
+        stream = stream if stream is not None else torch.cuda.current_stream()
+        rc = TimingEvent._hip.hipEventRecord(self.h, self._ct.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord failed: {rc}")
+
+    def elapsed_time(self, end):
+        ms = self._ct.c_float()
+        rc = TimingEvent._hip.hipEventElapsedTime(self._ct.byref(ms), self.h, end.h)
+        if rc != 0:
+            raise RuntimeError(f"hipEventElapsedTime failed: {rc}")
+        return ms.value
+
+    def __del__(self):
+        if TimingEvent._hip is not None and self.h:
+            TimingEvent._hip.hipEventDestroy(self.h)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -509,8 +546,9 @@ def main():
         if distributed:
             dist.barrier()
         torch.cuda.synchronize()
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+        evs = [[TimingEvent() for _ in range(3)] for _ in range(a.steps)]
         eraft_amd._lib.stage_events = stages = []   # split build: events around its two launches
+        eraft_amd._lib.stage_event = TimingEvent
         t0 = time.perf_counter()
         for k in range(a.steps):
             step(evs[k], last=k == a.steps - 1)
@@ -520,6 +558,7 @@ def main():
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         eraft_amd._lib.stage_events = None
+        eraft_amd._lib.stage_event = None
 
     if lean:
         if len(stages) != a.steps:

@@ -160,6 +160,7 @@ if _build_mode not in BUILD_MODES:
 # Timing hook (bench.py): when a list, every split build appends its (start, after the operand
 # pass, after the GEMM) HIP events, recorded on the launch stream.  Never changes a result.
 stage_events = None
+stage_event = None   # bench.py: the timing-event class for stage_events (default torch.cuda.Event)
 
 
 def set_build_mode(mode: str):
@@ -188,7 +189,8 @@ def build_pyramid(fmap1, fmap2, B, D, H, W, q_count, levels, off, what, mode=Non
         ws = torch.empty(nbytes.value, dtype=torch.uint8, device=fmap2.device)
         tm = stage_events
         if tm is not None:   # bench.py: HIP events on this stream around the two stages
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            mk = stage_event or (lambda: torch.cuda.Event(enable_timing=True))
+            ev = [mk() for _ in range(3)]
             ev[0].record()
         check(lib().ecorr_build_split_pack(fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, q_count,
                                            ws.data_ptr(), st), what)
