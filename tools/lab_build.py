@@ -445,6 +445,10 @@ PATCHES["qsnost"] = PATCHES["qs"] + [
     ("build.hip", "return __builtin_amdgcn_make_buffer_rsrc(P.lvl[L] + (int64_t)g0 * G, 0, gspan * G * 4, 0x00020000);",
      "return __builtin_amdgcn_make_buffer_rsrc(P.lvl[L] + (int64_t)g0 * G, 0, 0 * gspan, 0x00020000);"),
 ]
+# lookup output store cache policy (tree: nt = 2)
+for _pol in (0, 16, 18):
+    PATCHES[f"lkst{_pol}"] = [("lookup.hip", "sbase + (a * K + bb) * P.q_count * 4, 2);",
+                               f"sbase + (a * K + bb) * P.q_count * 4, {_pol});")]
 # the tree as it is (the baseline of an A/B against an edited tree)
 PATCHES["base"] = []
 # lookup windows staged one column per work item (b32 loads) instead of 8-byte column pairs
