@@ -78,9 +78,16 @@ class TimingEvent:
             raise RuntimeError(f"hipEventElapsedTime failed: {rc}")
         return ms.value
 
-    def __del__(self):
+    def destroy(self):
         if TimingEvent._hip is not None and self.h:
             TimingEvent._hip.hipEventDestroy(self.h)
+            self.h = self._ct.c_void_p()
+
+    def __del__(self):   # main() destroys them while the runtime is up; this is the fallback
+        try:
+            self.destroy()
+        except Exception:
+            pass
 
 
 def parse():
@@ -573,6 +580,9 @@ def main():
         look_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps / iters
     pack_ms = sum(e[0].elapsed_time(e[1]) for e in stages) / len(stages) if stages else 0.0
     gemm_ms = sum(e[1].elapsed_time(e[2]) for e in stages) / len(stages) if stages else build_ms
+    for ev in evs + stages:
+        for e in ev:
+            e.destroy()
     if distributed:
         t = torch.tensor([elapsed, build_ms, look_ms, pack_ms, gemm_ms], dtype=torch.float64,
                          device="cpu" if single else device)
