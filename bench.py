@@ -51,14 +51,38 @@ class TimingEvent:
     it does not write back and invalidate the caches between two kernels, which a default event
     (torch.cuda.Event) does -- about 5 us of idle GPU per record inside the timed region (rocprof
     trace, profiles/r03_final3). Timing only; the timed region is still closed by a synchronize.
-    Calls the HIP runtime torch has loaded (one runtime per process: libamdhip64.so.7 by soname)."""
+    Calls the HIP runtime torch has already loaded (its path read from /proc/self/maps, so no
+    second runtime can come in); TimingEvent.available() is False when it cannot be found, and the
+    bench then falls back to torch.cuda.Event."""
     _hip = None
     DISABLE_SYSTEM_FENCE = 0x20000000
 
+    @staticmethod
+    def _runtime_path():
+        try:
+            with open("/proc/self/maps") as f:
+                for line in f:
+                    path = line.split()[-1] if len(line.split()) >= 6 else ""
+                    if os.path.basename(path).startswith("libamdhip64.so"):
+                        return path
+        except OSError:
+            pass
+        return None
+
+    @classmethod
+    def available(cls):
+        if cls._hip is None:
+            import ctypes
+            path = cls._runtime_path()
+            if path is None:
+                return False
+            cls._hip = ctypes.CDLL(path)
+        return True
+
     def __init__(self):
         import ctypes
-        if TimingEvent._hip is None:
-            TimingEvent._hip = ctypes.CDLL("libamdhip64.so.7")
+        if not TimingEvent.available():
+            raise RuntimeError("the HIP runtime torch loaded is not mapped in this process")
         self._ct = ctypes
         self.h = ctypes.c_void_p()
         rc = TimingEvent._hip.hipEventCreateWithFlags(ctypes.byref(self.h), ctypes.c_uint(self.DISABLE_SYSTEM_FENCE))
@@ -88,6 +112,21 @@ class TimingEvent:
             self.destroy()
         except Exception:
             pass
+
+
+class TorchTimingEvent(torch.cuda.Event):
+    """torch.cuda.Event with TimingEvent's interface (the fallback when no HIP runtime is mapped)."""
+
+    def __init__(self):
+        super().__init__(enable_timing=True)
+
+    def destroy(self):
+        pass
+
+
+def timing_event():
+    """A fence-free HIP timing event, or torch's own where the runtime path cannot be resolved."""
+    return TimingEvent() if TimingEvent.available() else TorchTimingEvent()
 
 
 def parse():
@@ -553,9 +592,9 @@ def main():
         if distributed:
             dist.barrier()
         torch.cuda.synchronize()
-        evs = [[TimingEvent() for _ in range(3)] for _ in range(a.steps)]
+        evs = [[timing_event() for _ in range(3)] for _ in range(a.steps)]
         eraft_amd._lib.stage_events = stages = []   # split build: events around its two launches
-        eraft_amd._lib.stage_event = TimingEvent
+        eraft_amd._lib.stage_event = timing_event
         t0 = time.perf_counter()
         for k in range(a.steps):
             step(evs[k], last=k == a.steps - 1)

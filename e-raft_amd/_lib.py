@@ -98,12 +98,12 @@ def lib():
 
 
 def source_digest() -> str:
-    """sha256 (16 hex) of the kernel sources and the C header: ties a committed PMC summary
+    """sha256 (16 hex) of the kernel sources, their Makefile (flags) and the C header: ties a committed PMC summary
     (profiles/latest_pmc.json, tools/pmc_summary.py) to the code it measured."""
     import hashlib
     root = os.path.dirname(os.path.abspath(__file__))
     files = sorted(os.path.join(root, "csrc", f) for f in os.listdir(os.path.join(root, "csrc"))
-                   if f.endswith((".hip", ".h")))
+                   if f.endswith((".hip", ".h")) or f == "Makefile")   # the Makefile: compile flags
     files.append(os.path.join(root, "..", "include", "ecorr.h"))
     h = hashlib.sha256()
     for f in files:

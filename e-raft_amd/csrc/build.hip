@@ -19,9 +19,7 @@
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
 
-#include <atomic>
 #include <type_traits>
-#include <utility>
 
 namespace ecorr {
 
@@ -1121,478 +1119,6 @@ __global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
 }
 
 // ============================================================================================
-// Query-stationary persistent split GEMM (D = 256, four fused levels): build_qs_kernel.
-//
-// One block per CU (4 waves, one per SIMD) walks a contiguous range of (batch item, 256-query
-// tile, 128-target n-tile) units.  Each wave keeps its 64 queries' hi/lo fragments for the whole
-// K (8 chunk pairs x 4 groups x hi, lo = 256 registers) in AGPRs, loaded once per query tile, so
-// only the target panels move per unit: half an n-tile (64 targets, 64 KB) at a time, LDS-DMA'd
-// into one of two LDS buffers while the other one is in use.  The MFMAs of half n accumulate into
-// one 64-register set while the epilogue of half n - 1 runs from the other set, interleaved with
-// them three MFMAs at a time (one wave per SIMD has the vector issue slots an MFMA leaves free).
-//
-// Target order within a half (qs_target): lane (query qn, k block kb) of 16x16 tile (query group
-// g, target group tg) holds targets 16 tg + 4 kb + i, i = 0..3 -- 16 contiguous bytes of level-0
-// half-line tg (rows 2 (tg & 1), +1 of tile line tg >> 1; band: line = the 8-column tile), so the
-// four kb lanes of a query store one 64-byte half line per instruction (a 16-query x 64 B pattern
-// that runs at full store rate as non-temporal sc1 stores, tools/store_lab.hip quad64).  Level 1
-// pools across the lane pair kb, kb ^ 2 (lanes l, l ^ 32: v_permlane32_swap), level 2 across the
-// line's lanes, level 3 across kb = 0 / 1 (v_permlane16_swap); levels 2-3 of a unit are gathered
-// in a wave-private LDS staging area and leave as whole rows when the unit's second half is done.
-//
-// Memory-op ordering: a wave's vector-memory ops per half are [next half's DMA (+ its target
-// exponents on wave 0)] then the previous half's epilogue stores (>= 24), so waiting for a half's
-// panel is vmcnt(24) (a query-tile change drains vmcnt(0) once).
-// ============================================================================================
-#define QS_INLINE __attribute__((always_inline))   // every helper lambda of build_qs_kernel
-// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): compile-time steps, so each
-// step's code is instantiated on its own (a plain unrolled loop over the 128 interleaved steps
-// exceeded the unroller's budget and left the query fragments dynamically indexed, in scratch)
-template <typename F, int... I>
-__device__ __forceinline__ void qs_static_for(F&& f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void qs_static_for(F&& f) {
-    qs_static_for(f, std::make_integer_sequence<int, N>{});
-}
-constexpr int QS_HCP = 4 * 2048;                  // bytes of a 64-target half panel per chunk pair
-constexpr int QS_HALF = NCP * QS_HCP;             // 64 KB: one half's whole K
-constexpr int QS_STG = 64 * 8 * 4 + 64 * 2 * 4 + 16;   // per wave: L2 staging [64][8] + L3 [64][2] floats + a dummy slot
-constexpr int QS_LDS = 2 * QS_HALF + 4 * QS_STG + 3 * 64 * 8;   // panels, staging, 3 target-exponent slots
-constexpr int QS_NST = 24;                        // epilogue stores per half before any flush
-constexpr int QS_ST = 18;                         // nt | sc1: half-line stores at full rate
-constexpr int FOOB_QS = 0x40000000;               // beyond every slab: + a lane part, or twice, stays >= any range
-
-// target (y, x) of position p (0..127) of a qs fmap2 panel, relative to the n-tile origin
-__host__ __device__ __forceinline__ void qs_target(int p, bool band, int& y, int& x) {
-    const int h = p >> 6, tg = (p >> 4) & 3, kb = (p >> 2) & 3, i = p & 3;
-    if (!band) {
-        y = 2 * tg + (kb >> 1);
-        x = 8 * h + 4 * (kb & 1) + i;
-    } else {
-        y = 2 * (tg & 1) + (kb >> 1);
-        x = 16 * h + 8 * (tg >> 1) + 4 * (kb & 1) + i;
-    }
-}
-// ... and its inverse (the pack kernel's fmap2 positions)
-__device__ __forceinline__ int qs_pos(int y, int x, bool band) {
-    if (!band) return 64 * (x >> 3) + 16 * (y >> 1) + 4 * (2 * (y & 1) + ((x & 7) >> 2)) + (x & 3);
-    const int xx = x & 15;
-    return 64 * (x >> 4) + 16 * (2 * (xx >> 3) + (y >> 1)) + 4 * (2 * (y & 1) + ((xx & 7) >> 2)) + (xx & 3);
-}
-
-// what the epilogue of one half needs, fixed when that half's MFMAs end (the rest -- buffer
-// descriptors, line and block offsets -- is rederived from it by scalar ops where used)
-struct QsCtx {
-    float sq[4];              // 2^-(e_q + 4) per query group (fast) / that exponent as bits (slow)
-    int qfast;                // every query exponent of the wave in [-63, 63]
-    int rows0, nq;            // first query row of the tile (slab-wide), valid queries in it
-    int ty0, tx0, band, h;    // the n-tile and the half
-    int slot;                 // target-exponent slot
-};
-
-template <bool MUL>
-__global__ __launch_bounds__(256, 1) void build_qs_kernel(BuildParams P, int units) {
-    static_assert(MUL, "D = 256 only: 1/sqrt(D) = 2^-4");
-    __shared__ __attribute__((aligned(16))) char smem[QS_LDS];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int qn = lane & 15, kb = lane >> 4;
-    // the block's unit sequence s = 0 .. ue - 1: R full rounds in lockstep -- round r is query tile
-    // r G + block, n-tiles 0 .. n_nt - 1 in order, so at any time every block reads the same n-tile
-    // panel of its batch (L2 / MALL hits; with each block on its own n-tile phase the panels came
-    // from HBM again per query tile: 1.6 GB) -- then an even contiguous share of the rest
-    const int G = gridDim.x, NQT = units / P.n_nt, R = NQT / G;
-    const int Ur = (NQT - R * G) * P.n_nt;
-    const int rb = (int)((int64_t)blockIdx.x * Ur / G), re = (int)((int64_t)(blockIdx.x + 1) * Ur / G);
-    const int ub = 0, ue = R * P.n_nt + re - rb;
-    if (ub >= ue) return;   // block-uniform
-    char* const stg = smem + 2 * QS_HALF + wave * QS_STG;                          // [64][8] L2, then [64][2] L3
-    float* const xf = reinterpret_cast<float*>(smem + 2 * QS_HALF + 4 * QS_STG);   // [3][64] 2^-e_t (clamped)
-    int* const xe = reinterpret_cast<int*>(xf + 3 * 64);                           // [3][64] -e_t
-    const int64_t Q2 = (int64_t)P.H * P.W;
-    const int64_t pstride = (int64_t)NCP * PANEL16;   // bytes of one 128-pixel tile's panels
-    const int l0stride = (int)P.lsz[0] * 4;
-    const int nbx1 = -P.lntx[1], nbx2 = -P.lntx[2], nbx3 = -P.lntx[3];
-
-    struct Unit { int b, qt, nt; };
-    auto decode = [&](int s) QS_INLINE {
-        Unit t;
-        const int lin = s < R * P.n_nt ? (s / P.n_nt * G + (int)blockIdx.x) * P.n_nt + s % P.n_nt
-                                       : R * G * P.n_nt + rb + (s - R * P.n_nt);
-        t.nt = lin % P.n_nt;
-        const int r = lin / P.n_nt;
-        t.qt = r % P.n_qt;
-        t.b = r / P.n_qt;
-        return t;
-    };
-
-    // ---- query fragments (AGPRs) and exponents of the current query tile
-    halfx8 qh[NCP][4], ql[NCP][4];
-    int eq[4] = {0, 0, 0, 0};
-    auto load_queries = [&](const Unit& t) QS_INLINE {
-        const int qp = 2 * t.qt, nqp = min(2, P.n_mt - qp);
-        const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<char*>(P.pk1 + ((int64_t)t.b * P.n_mt + qp) * pstride), 0, (int)(nqp * pstride), 0x00020000);
-        const int qgo = (wave >> 1) * (int)pstride + (wave & 1) * (4 * 2048) + lane * 16;
-#pragma unroll
-        for (int cp = 0; cp < NCP; ++cp)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                qh[cp][g] = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(rq, qgo, cp * PANEL16 + g * 2048, 0));
-                ql[cp][g] = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(rq, qgo + 1024, cp * PANEL16 + g * 2048, 0));
-            }
-        const int q0 = t.qt * SQ;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int q = q0 + 64 * wave + 16 * g + qn;
-            eq[g] = q < P.q_count ? P.ex1[(int64_t)t.b * P.q_count + q] : 0;
-        }
-    };
-
-    // the fragments into their AGPRs here, then wait states: hipcc sees the MFMAs only as inline asm,
-    // so it neither keeps a v_accvgpr_write away from the MFMA that reads its AGPR nor pads the two
-    // (copies placed right before the first MFMAs fed stale B operands: a wrong first target group)
-    auto pin_queries = [&]() QS_INLINE {
-#pragma unroll
-        for (int cp = 0; cp < NCP; ++cp)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) asm volatile("" : "+a"(qh[cp][g]), "+a"(ql[cp][g]));
-        asm volatile("s_nop 7");
-    };
-
-    // ---- target panel half (u, h) -> LDS buffer `buf` (16 x 1 KB LDS-DMA per wave) and, on wave 0,
-    // the half's 64 target exponents -> et
-    int et = 0;
-    auto issue_half = [&](int u, int h, int buf) QS_INLINE {
-        const Unit t = decode(u);
-        const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<char*>(P.pk2 + ((int64_t)t.b * P.n_nt + t.nt) * pstride), 0, (int)pstride, 0x00020000);
-        char* const dst = smem + buf * QS_HALF;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const int pi = wave + 4 * s, cp = pi >> 3, c = pi & 7;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + cp * QS_HCP + c * 1024),
-                                                     16, lane * 16, cp * PANEL16 + h * 8192 + c * 1024, 0, 0);
-        }
-        if (wave == 0) {
-            const NTile tc = ntile_of(P, t.nt);
-            int y, x;
-            qs_target(64 * h + lane, tc.band, y, x);
-            y += tc.ty0;
-            x += tc.tx0;
-            et = (y < P.H && x < P.W) ? P.ex2[(int64_t)t.b * Q2 + (int64_t)y * P.W + x] : 0;
-        }
-    };
-    auto publish_exps = [&](int slot) QS_INLINE {   // wave 0, after the half's wait
-        if (wave == 0) {
-            xe[slot * 64 + lane] = -et;
-            xf[slot * 64 + lane] = exp2i(max(-63, min(-et, 63)));
-        }
-    };
-
-    // ---- epilogue context of half (u, h)
-    QsCtx C;
-    auto make_ctx = [&](int u, int h, int slot) QS_INLINE {
-        const Unit t = decode(u);
-        const NTile tc = ntile_of(P, t.nt);
-        const int q0 = t.qt * SQ;
-        C.rows0 = t.b * P.q_count + q0;
-        C.nq = min(SQ, P.q_count - q0);
-        C.ty0 = tc.ty0;
-        C.tx0 = tc.tx0;
-        C.band = tc.band;
-        C.h = h;
-        C.slot = slot;
-        bool qf = true;
-        int nqe[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            nqe[g] = -(eq[g] + P.scale_shift);
-            qf &= nqe[g] >= -63 && nqe[g] <= 63;
-        }
-        C.qfast = __all(qf);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) C.sq[g] = C.qfast ? exp2i(nqe[g]) : __int_as_float(nqe[g]);
-    };
-    // buffer descriptors of the fused levels for the context's query tile: level 0 over its query
-    // images, levels 1-3 over its 64-row groups
-    auto lvl_rsrc = [&](int L) QS_INLINE {
-        if (L == 0)
-            return __builtin_amdgcn_make_buffer_rsrc(P.lvl[0] + (int64_t)C.rows0 * P.lsz[0], 0, C.nq * l0stride, 0x00020000);
-        const int g0 = C.rows0 >> 6, gspan = ((C.rows0 + C.nq - 1) >> 6) - g0 + 1;
-        const int G = kGroup * (int)P.lsz[L];
-        return __builtin_amdgcn_make_buffer_rsrc(P.lvl[L] + (int64_t)g0 * G, 0, gspan * G * 4, 0x00020000);
-    };
-    // byte offset of query row `qlw` (wave-local 64 wave + ...) in interleaved level L's group slab
-    // (piece `pc` floats into the row), FOOB_QS past the tile's valid queries
-    auto ilv_row = [&](int L, int qlw, int pc) QS_INLINE {
-        const int R = C.rows0 + qlw, g0 = C.rows0 >> 6;
-        const int G = kGroup * (int)P.lsz[L], rowf = L == 3 ? 2 : 8;
-        return qlw < C.nq ? (((R >> 6) - g0) * G + (R & 63) * rowf + pc) * 4 : FOOB_QS;
-    };
-    // level-0 half-line tg of the context's half: byte offset in a query image (FOOB_QS outside)
-    auto l0_line = [&](int tg) QS_INLINE {
-        const int tr0 = C.ty0 >> 2, tc0 = C.tx0 >> 3;
-        const int tr = C.band ? tr0 : tr0 + (tg >> 1);
-        const int tcc = C.band ? tc0 + 2 * C.h + (tg >> 1) : tc0 + C.h;
-        return (tr < P.lnty[0] && tcc < P.lntx[0]) ? ((tr * P.lntx[0] + tcc) * kTile + 16 * (tg & 1)) * 4 : FOOB_QS;
-    };
-    // level-1 block of line ln of the context's half: byte offset of the block (FOOB_QS outside)
-    auto l1_block = [&](int ln) QS_INLINE {
-        const int tr0 = C.ty0 >> 2, tc0 = C.tx0 >> 3;
-        const int by = C.band ? tr0 : tr0 + ln;
-        const int bx = C.band ? tc0 + 2 * C.h + ln : tc0 + C.h;
-        return (by < P.lnty[1] && bx < nbx1) ? (by * nbx1 + bx) * kGroup * 8 * 4 : FOOB_QS;
-    };
-
-    // ---- MFMAs (inline asm, accumulators in VGPRs, query fragments in AGPRs)
-    floatx4 acc0[4][4], acc1[4][4];
-    auto mfma = [&](floatx4& c, const halfx8& a, const halfx8& b) QS_INLINE {
-        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
-    };
-    auto mfma0 = [&](floatx4& c, const halfx8& a, const halfx8& b) QS_INLINE {   // c = a b (first chunk pair)
-        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "a"(b));
-    };
-    struct AF { halfx8 h, l; };
-    auto read_a = [&](int buf, int cp, int tg, AF& a) QS_INLINE {
-        const char* p = smem + buf * QS_HALF + cp * QS_HCP + tg * 2048 + lane * 16;
-        a.h = *reinterpret_cast<const halfx8*>(p);
-        a.l = *reinterpret_cast<const halfx8*>(p + 1024);
-    };
-
-    // ---- epilogue state of the half being finished
-    floatx4 st[4];     // its target factors (fast) / negated exponents as bits (slow)
-    int tfast = 1;
-    floatx4 v;         // the current (query group, target group)'s scaled values
-    float p1[4];       // level-1 pixels of the current query group, per target group
-    float cd[2];       // the partner row's two values of the current level-1 pixel
-    float l2v[2];      // level-2 pixels (lanes kb < 2) per line
-    float sw1x[2], sw1y[2];   // the level-1 store swap per line (kept for level 2)
-    // store addressing of the half being finished (rows0 % 64 == 0, launch_build's condition):
-    // offset = a lane constant (its query row qn of the 16-query group, its piece kb) + a
-    // wave-uniform term (query group, line / block, the wave's 64-row group) -- one v_add per store
-    __amdgpu_buffer_rsrc_t er0, er1;
-    int eu0[4], eu1[2];
-    const int l0lane = qn * l0stride + 16 * kb, l1lane = (qn * 8 + 2 * kb) * 4;
-    auto epi_begin = [&]() QS_INLINE {
-        er0 = lvl_rsrc(0);
-        er1 = lvl_rsrc(1);
-        const int G1 = kGroup * (int)P.lsz[1] * 4;
-#pragma unroll
-        for (int tg = 0; tg < 4; ++tg) eu0[tg] = __builtin_amdgcn_readfirstlane(l0_line(tg) + 64 * wave * l0stride);
-#pragma unroll
-        for (int ln = 0; ln < 2; ++ln) eu1[ln] = __builtin_amdgcn_readfirstlane(l1_block(ln) + wave * G1);
-        const float* s = C.qfast ? xf + C.slot * 64 : reinterpret_cast<const float*>(xe + C.slot * 64);
-#pragma unroll
-        for (int tg = 0; tg < 4; ++tg) st[tg] = *reinterpret_cast<const floatx4*>(s + 16 * tg + 4 * kb);
-        bool ok = true;
-        if (C.qfast) {
-            const int* e = xe + C.slot * 64;
-#pragma unroll
-            for (int tg = 0; tg < 4; ++tg) {
-                const int4 e4 = *reinterpret_cast<const int4*>(e + 16 * tg + 4 * kb);
-                ok &= e4.x >= -63 && e4.x <= 63 && e4.y >= -63 && e4.y <= 63 && e4.z >= -63 && e4.z <= 63 &&
-                      e4.w >= -63 && e4.w <= 63;
-            }
-        }
-        tfast = C.qfast && __all(ok);
-        if (C.qfast && !tfast) {   // the slow path reads the exponents instead
-            const float* s2 = reinterpret_cast<const float*>(xe + C.slot * 64);
-#pragma unroll
-            for (int tg = 0; tg < 4; ++tg) st[tg] = *reinterpret_cast<const floatx4*>(s2 + 16 * tg + 4 * kb);
-        }
-    };
-    // one epilogue micro-step: step k (0..127) of the half whose accumulators are A.  Per query group
-    // g (32 steps): per target group tg five steps -- scale two values, two values, the level-0
-    // half-line store, the level-1 pixel (two steps) -- then the two level-1 line stores, the two
-    // level-2 pixels (two steps each), the level-3 pixel
-    auto epi_step = [&](floatx4 (&A)[4][4], auto kc, auto fast_c) QS_INLINE {
-        constexpr int k = decltype(kc)::value;
-        constexpr bool FAST = decltype(fast_c)::value;
-        constexpr int g = k >> 5, m = k & 31;
-        if constexpr (m < 20) {
-            constexpr int tg = m / 5, ms = m % 5;
-            if constexpr (ms < 2) {   // scale values 2 ms, 2 ms + 1
-                if constexpr (FAST) {
-                    const floatx2 f = floatx2{C.sq[g], C.sq[g]} * floatx2{st[tg][2 * ms], st[tg][2 * ms + 1]};
-                    const floatx2 x = floatx2{A[g][tg][2 * ms], A[g][tg][2 * ms + 1]} * f;
-                    v[2 * ms] = x[0];
-                    v[2 * ms + 1] = x[1];
-                } else {
-                    const int n = __float_as_int(C.sq[g]);
-                    v[2 * ms] = ldexpf(A[g][tg][2 * ms], n + __float_as_int(st[tg][2 * ms]));
-                    v[2 * ms + 1] = ldexpf(A[g][tg][2 * ms + 1], n + __float_as_int(st[tg][2 * ms + 1]));
-                }
-            } else if constexpr (ms == 2) {   // level-0 half line (range-checked per query image by the descriptor)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), er0,
-                                                       l0lane + (eu0[tg] + 16 * g * l0stride), 0, QS_ST);
-            } else if constexpr (ms == 3) {
-                // lanes < 32 (level-0 row 0 of the half line): a, b = own v0, v1, c, d = row 1's v0, v1;
-                // lanes >= 32: a, b = row 0's v2, v3, c, d = own v2, v3
-                const auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0]), __float_as_uint(v[2]), false, false);
-                const auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[1]), __float_as_uint(v[3]), false, false);
-                p1[tg] = __fadd_rn(__uint_as_float(s0[0]), __uint_as_float(s1[0]));
-                cd[0] = __uint_as_float(s0[1]);
-                cd[1] = __uint_as_float(s1[1]);
-            } else {
-                p1[tg] = __fmul_rn(__fadd_rn(__fadd_rn(p1[tg], cd[0]), cd[1]), 0.25f);
-            }
-        } else if constexpr (m < 22) {   // level-1 store of line m - 20: lane kb -> block floats 2 kb, 2 kb + 1
-            constexpr int ln = m - 20;
-            const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(p1[2 * ln]), __float_as_uint(p1[2 * ln + 1]), false, false);
-            sw1x[ln] = __uint_as_float(s[0]);
-            sw1y[ln] = __uint_as_float(s[1]);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, floatx2{sw1x[ln], sw1y[ln]}), er1,
-                                                  l1lane + (eu1[ln] + 16 * g * 8 * 4), 0, QS_ST);
-        } else if constexpr (m < 26) {   // level-2 pixel of line (m - 22) >> 1 on lanes kb < 2 (two steps)
-            constexpr int ln = (m - 22) >> 1;
-            if constexpr (((m - 22) & 1) == 0) {
-                // lanes kb < 2: a = own P(0, 2 kb) = sw1x, b = P(0, 2 kb + 1) = sw1y, c = own P(1, 2 kb) =
-                // p1[2 ln + 1], d = P(1, 2 kb + 1) from lane + 32 (its sw1y)
-                const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(sw1y[ln]), __float_as_uint(sw1y[ln]), false, false);
-                l2v[ln] = __fadd_rn(__fadd_rn(sw1x[ln], sw1y[ln]), p1[2 * ln + 1]);
-                sw1x[ln] = __uint_as_float(s[1]);
-            } else {
-                l2v[ln] = __fmul_rn(__fadd_rn(l2v[ln], sw1x[ln]), 0.25f);
-                // staging: regular [q][ln * 4 + 2 h + kb]; band [q][2 ln + kb] (the half's block row)
-                const int col = C.band ? 2 * ln + kb : ln * 4 + 2 * C.h + kb;
-                float* dst = reinterpret_cast<float*>(stg) + (kb < 2 ? (16 * g + qn) * 8 + col : 64 * 8 + 2 * 64);
-                *dst = l2v[ln];
-            }
-        } else if constexpr (m == 26) {   // level 3 (regular): pool of the 2 x 2 level-2 pixels, lane kb = 0
-            if (!C.band) {
-                const auto s0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l2v[0]), __float_as_uint(l2v[0]), false, false);
-                const auto s1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l2v[1]), __float_as_uint(l2v[1]), false, false);
-                const float p3 = pool4(l2v[0], __uint_as_float(s0[1]), l2v[1], __uint_as_float(s1[1]));
-                float* dst = reinterpret_cast<float*>(stg) + (kb == 0 ? 64 * 8 + (16 * g + qn) * 2 + C.h : 64 * 8 + 2 * 64);
-                *dst = p3;
-            }
-        }
-        // m 27..31: free
-    };
-    // levels 2-3 from the staging area to their rows (regular: after the unit's second half;
-    // band: level 2 after every half); wave-private LDS, in program order
-    auto flush = [&]() QS_INLINE {
-        const float* s = reinterpret_cast<const float*>(stg);
-        const int by2 = C.ty0 >> 3, bx2 = (C.tx0 >> 4) + (C.band ? C.h : 0);
-        const bool ok2 = by2 < P.lnty[2] && bx2 < nbx2;
-        const int blk2 = ok2 ? (by2 * nbx2 + bx2) * kGroup * 8 * 4 : FOOB_QS;
-        if (!C.band) {
-            if (C.h != 1) return;
-            const int by3 = C.ty0 >> 3, bx3 = C.tx0 >> 4;
-            const bool ok3 = by3 < P.lnty[3] && bx3 < nbx3;
-            const int blk3 = ok3 ? (by3 * nbx3 + bx3) * kGroup * 2 * 4 : FOOB_QS;
-#pragma unroll
-            for (int part = 0; part < 2; ++part) {
-                const int q = (lane >> 1) + 32 * part;
-                const floatx4 x = *reinterpret_cast<const floatx4*>(s + q * 8 + 4 * (lane & 1));
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, x), lvl_rsrc(2),
-                                                       ilv_row(2, 64 * wave + q, 4 * (lane & 1)) + blk2, 0, QS_ST);
-            }
-            const floatx2 x3 = *reinterpret_cast<const floatx2*>(s + 64 * 8 + lane * 2);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, x3), lvl_rsrc(3),
-                                                  ilv_row(3, 64 * wave + lane, 0) + blk3, 0, QS_ST);
-        } else {
-            const int r2 = (C.ty0 >> 2) & 1;
-            const floatx4 x = *reinterpret_cast<const floatx4*>(s + lane * 8);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, x), lvl_rsrc(2),
-                                                   ilv_row(2, 64 * wave + lane, 4 * r2) + blk2, 0, QS_ST);
-        }
-    };
-
-    // ---- one half: wait for its panel, publish its exponents, start the next half's transfer, then
-    // its MFMAs (buffer / accumulators PAR) interleaved with the previous half's epilogue
-    int hs = 0;   // halves begun by this block (the exponent slot is hs % 3)
-    // FAST: the half being finished takes the power-of-two scaling path (tfast, decided by epi_begin
-    // before the call: one branch per half, not one per scaling step)
-    auto run_half = [&](auto par_c, auto mf_c, auto epi_c, auto wait_c, auto fast_c, int u, int h) QS_INLINE {
-        constexpr int PAR = decltype(par_c)::value;
-        constexpr bool MF = decltype(mf_c)::value, EPI = decltype(epi_c)::value;
-        constexpr int WAITN = decltype(wait_c)::value;
-        floatx4 (&AM)[4][4] = PAR == 0 ? acc0 : acc1;   // MFMA target
-        floatx4 (&AE)[4][4] = PAR == 0 ? acc1 : acc0;   // the previous half's results
-        (void)AM;
-        (void)AE;
-        if constexpr (MF) {
-            wait_vm<WAITN, true>();
-            publish_exps(hs % 3);
-            wait_vm<63, true>();   // the exponents are in LDS (lgkmcnt only: the queued stores stay queued)
-            __builtin_amdgcn_s_barrier();
-            // the next half: (u, 1) or (u + 1, 0)
-            const int un = h == 0 ? u : u + 1, hn = h ^ 1;
-            if (un < ue) issue_half(un, hn, PAR ^ 1);
-        }
-        AF af[2];
-        if constexpr (MF) read_a(PAR, 0, 0, af[0]);
-        qs_static_for<NCP * 16>([&](auto kc) QS_INLINE {
-            constexpr int k = decltype(kc)::value;
-            constexpr int cp = k >> 4, tg = (k >> 2) & 3, j = k & 3, s4 = k >> 2;
-            if constexpr (MF) {
-                if constexpr (j == 0) {   // the next target group's fragments, one group ahead
-                    if constexpr (tg < 3) read_a(PAR, cp, tg + 1, af[(s4 + 1) & 1]);
-                    else if constexpr (cp + 1 < NCP) read_a(PAR, cp + 1, 0, af[(s4 + 1) & 1]);
-                }
-                // MFMAs 3 j .. 3 j + 2 of the group's twelve: hh, lh per query group, then hl x4
-                // (build_split16_kernel's order: every accumulator sums hh, lh, hl, so the two
-                // builds agree bitwise)
-                const AF& a = af[s4 & 1];
-                qs_static_for<3>([&](auto ic) QS_INLINE {
-                    constexpr int n = 3 * j + decltype(ic)::value;
-                    constexpr int g = n < 8 ? n >> 1 : n - 8, kind = n < 8 ? n & 1 : 2;
-                    const halfx8& av = kind == 1 ? a.l : a.h;
-                    const halfx8& bv = kind == 2 ? ql[cp][g] : qh[cp][g];
-                    if constexpr (cp == 0 && kind == 0) mfma0(AM[g][tg], av, bv);
-                    else mfma(AM[g][tg], av, bv);
-                });
-            }
-            if constexpr (EPI) epi_step(AE, kc, fast_c);
-            __builtin_amdgcn_sched_barrier(0);
-        });
-        if constexpr (EPI) flush();
-        if constexpr (MF) {
-            // the MFMA results are read by the next half's epilogue VALU: pad the XDL -> VALU distance
-            asm volatile("s_nop 15");
-            asm volatile("s_nop 15");
-            make_ctx(u, h, hs % 3);
-            ++hs;
-        }
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using BT = std::true_type;
-    using BF = std::false_type;
-    using W0 = std::integral_constant<int, 0>;
-    using WN = std::integral_constant<int, QS_NST>;
-
-    Unit cur = decode(ub);
-    load_queries(cur);
-    issue_half(ub, 0, 0);
-    pin_queries();
-    // a half with an epilogue: its scaling path chosen once
-    auto run_epi = [&](auto par_c, auto mf_c, auto wait_c, int u, int h) QS_INLINE {
-        epi_begin();
-        if (tfast) run_half(par_c, mf_c, BT(), wait_c, BT(), u, h);
-        else run_half(par_c, mf_c, BT(), wait_c, BF(), u, h);
-    };
-    run_half(I0(), BT(), BF(), W0(), BT(), ub, 0);
-    run_epi(I1(), BT(), W0(), ub, 1);
-    for (int u = ub + 1; u < ue; ++u) {
-        const Unit t = decode(u);
-        if (t.b != cur.b || t.qt != cur.qt) {   // a new query tile: drain, then reload (rare)
-            cur = t;
-            wait_vm<0, true>();
-            load_queries(cur);
-            pin_queries();
-        }
-        run_epi(I0(), BT(), WN(), u, 0);
-        run_epi(I1(), BT(), WN(), u, 1);
-    }
-    run_epi(I0(), BF(), W0(), ue, 0);   // the last half's epilogue alone
-}
-
-// ============================================================================================
 // fp32 GEMM for D = 256 (ecorr_build): build_split_kernel's structure -- 256 x 128 block tile, 4
 // waves of 64 queries x 128 targets, two blocks per CU, the register epilogue split_epilogue() --
 // on v_mfma_f32_32x32x2_f32 with the fp32 operands read straight from the fmaps (no operand pass):
@@ -1804,7 +1330,7 @@ __device__ __forceinline__ void split_f16(const float (&v)[8], float s, halfx8& 
 // L16: the panel layout of build_split16_kernel (16 KB per 128-pixel tile and 32-deep chunk pair:
 // [16-pixel group g][hi | lo][k block kb][pixel r][8 halves], k = 8 kb + j within the pair; fmap2
 // positions in split16_target order) instead of build_split_kernel's 8-KB chunk panels.
-template <bool ISB, bool L16, bool QS = false>
+template <bool ISB, bool L16>
 __device__ __forceinline__ void pack_body(const float* __restrict__ x, const BuildParams& P, int* __restrict__ ex,
                                           char* __restrict__ pack) {
     __shared__ float red[4][64];
@@ -1835,8 +1361,7 @@ __device__ __forceinline__ void pack_body(const float* __restrict__ x, const Bui
             // groups of the panel (256-byte runs per store); otherwise rows 2 r4, 2 r4 + 1
             y = L16 ? r4 + 4 * (l >> 5) : 2 * r4 + (l >> 5);
             x = l & 15;
-            pos = QS ? qs_pos(y, x, false)
-                : L16 ? 16 * (2 * (y & 3) + ((x >> 2) & 1)) + 4 * ((y >> 2) | ((x >> 3) << 1)) + (x & 3)
+            pos = L16 ? 16 * (2 * (y & 3) + ((x >> 2) & 1)) + 4 * ((y >> 2) | ((x >> 3) << 1)) + (x & 3)
                       : 64 * (x >> 3) + 32 * (y >> 2) + 8 * (y & 3) + (x & 7);
         } else {
             const int bb = blockIdx.x - nreg_blk;
@@ -1844,8 +1369,7 @@ __device__ __forceinline__ void pack_body(const float* __restrict__ x, const Bui
             ok = tile < P.n_nt;
             y = 2 * (bb & 1) + (l >> 5);
             x = l & 31;
-            pos = QS ? qs_pos(y, x, true)
-                : L16 ? 16 * (2 * y + ((x >> 2) & 1)) + 4 * (x >> 3) + (x & 3) : 32 * (x >> 3) + 8 * y + (x & 7);
+            pos = L16 ? 16 * (2 * y + ((x >> 2) & 1)) + 4 * (x >> 3) + (x & 3) : 32 * (x >> 3) + 8 * y + (x & 7);
         }
         const NTile n = ntile_of(P, ok ? tile : 0);
         live = ok;
@@ -1917,13 +1441,12 @@ __device__ __forceinline__ void pack_body(const float* __restrict__ x, const Bui
 // tiles), z = 1 fmap2 (n-tiles).  Neither pass alone fills the chip; one grid overlaps the two and
 // drops a launch boundary (round-1 A/B, profiles/r01_final8/ab_pack.txt).  Surplus x blocks of the
 // shorter pass return at once (block-uniform, before pack_body's barrier).
-// QS: fmap2 panels in build_qs_kernel's target order (qs_target); fmap1 panels are the same.
-template <bool L16, bool QS = false>
+template <bool L16>
 __global__ __launch_bounds__(256) void pack_both_kernel(BuildParams P) {
     if (blockIdx.z == 0) {
         if ((int)blockIdx.x < 2 * P.n_mt) pack_body<false, L16>(P.f1, P, P.ex1, const_cast<char*>(P.pk1));
     } else if ((int)blockIdx.x < 4 * (P.n_reg / P.n_ntx) * ((P.n_ntx + 1) / 2) + 2 * (P.n_nt - P.n_reg)) {
-        pack_body<true, L16, QS>(P.f2, P, P.ex2, const_cast<char*>(P.pk2));
+        pack_body<true, L16>(P.f2, P, P.ex2, const_cast<char*>(P.pk2));
     }
 }
 
@@ -2371,23 +1894,6 @@ int64_t build_split_workspace_bytes(int B, int D, int H, int W, int q_count) {
     return split_ws(P, B).total;
 }
 
-namespace {
-// the query-stationary build (build_qs_kernel) in place of build_split16_kernel
-constexpr bool kBuildQS = false;
-// compute units of the current device (cached per device ordinal; 256 on MI355X)
-int device_cus() {
-    static std::atomic<int> cache[64];   // zero-initialized: 0 = not queried yet
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    int n = cache[dev].load(std::memory_order_relaxed);
-    if (n == 0) {
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cache[dev].store(n, std::memory_order_relaxed);
-    }
-    return n;
-}
-}  // namespace
-
 int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid, hipStream_t stream, int stages) {
     BuildParams P = P0;
     const int levels = g.levels;
@@ -2416,15 +1922,10 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
         P.pk2 = P.ws + w.pk2;
         const int nx2 = 4 * (P.n_reg / P.n_ntx) * ((P.n_ntx + 1) / 2) + 2 * (P.n_nt - P.n_reg);   // fmap2 blocks
         const int nx = 2 * P.n_mt > nx2 ? 2 * P.n_mt : nx2;
-        // D = 256: build_split16_kernel and its panel layout (or the query-stationary build_qs_kernel
-        // and its own fmap2 order -- decided from D alone: the pack stage does not know the levels;
-        // level 0 is always tiled and levels 1-3 interleaved, and absent levels have empty buffer
-        // ranges); other D: build_split_kernel
+        // D = 256: build_split16_kernel and its panel layout; other D: build_split_kernel
         const bool s16 = (P.D + 15) / 16 == 2 * NCP;
-        const bool qs = kBuildQS && s16 && P.scale_is_mul && P.q_count % kGroup == 0;
         if (stages & 1) {
-            if (qs) hipLaunchKernelGGL((pack_both_kernel<true, true>), dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
-            else if (s16) hipLaunchKernelGGL((pack_both_kernel<true>), dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
+            if (s16) hipLaunchKernelGGL((pack_both_kernel<true>), dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
             else hipLaunchKernelGGL((pack_both_kernel<false>), dim3((unsigned)nx, B, 2), dim3(256), 0, stream, P);
         }
         if (!(stages & 2)) {
@@ -2432,10 +1933,7 @@ int launch_build(const BuildParams& P0, int B, const PyrGeom& g, float* pyramid,
             return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
         }
         const dim3 grid((unsigned)ntiles);
-        if (qs) {   // one block per CU, each a contiguous range of (batch, query tile, n-tile) units
-            const int g = (int)std::min<int64_t>(ntiles, device_cus());
-            hipLaunchKernelGGL((build_qs_kernel<true>), dim3((unsigned)g), dim3(256), 0, stream, P, (int)ntiles);
-        } else if (s16) {
+        if (s16) {
             if (P.scale_is_mul) hipLaunchKernelGGL((build_split16_kernel<true>), grid, dim3(256), 0, stream, P);
             else hipLaunchKernelGGL((build_split16_kernel<false>), grid, dim3(256), 0, stream, P);
         } else {

@@ -27,6 +27,14 @@ def _free_port():
 
 
 def test_two_rank_batch_shard():
+    # Precondition: this process has not initialised the GPU.  The launcher is a forked child of
+    # the pytest process; a child that execs from a GPU-initialised parent can take the machine
+    # down on this pool.  conftest.py orders this test first in the session; if a reordering ever
+    # runs a GPU test before it, fail here instead of spawning the ranks.
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():
+        pytest.fail("test_two_rank_batch_shard must run before any test initialises the GPU in this "
+                    "process (conftest.py puts it first); run it alone: pytest tests/test_batch_shard_gpu.py")
     steps, B = 2, 16
     env = dict(os.environ, BENCH_SINGLE_DEVICE="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",

@@ -27,7 +27,8 @@ def source_digest():
     import hashlib
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     csrc = os.path.join(repo, "e-raft_amd", "csrc")
-    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".hip", ".h")))
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc)
+                   if f.endswith((".hip", ".h")) or f == "Makefile")   # the Makefile: compile flags
     files.append(os.path.join(repo, "include", "ecorr.h"))
     h = hashlib.sha256()
     for f in files:
