@@ -1,0 +1,29 @@
+#!/bin/bash
+# One lab call: optional GPU suite / bench, then A/Bs of lab builds against the tree.
+#   RUN_TESTS=1 RUN_BENCH=1 AB="name1 name2" ABT="timing-only names" LK="lookup lab names" tools/gpu_lab.sh TAG
+# AB: bitwise-checked build A/Bs (each alone vs the tree); ABT: timing-only build A/Bs (no check);
+# LK: lookup A/Bs (tools/ab_lookup.py, bitwise-checked).  Every step under its own time limit,
+# chained: the first failure ends the call.
+cd "$GRAFT_REPO_ROOT"; TAG=${1:-lab}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+if [ -n "$RUN_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; grep -E 'FAILED|ERROR|passed|failed' $OUT/pytest_gpu.log | tail -5; [ $rc -ne 0 ] && exit $rc
+fi
+if [ -n "$RUN_BENCH" ]; then
+  timeout -k 10 400 python -u bench.py $BENCH_ARGS > $OUT/bench.log 2>&1
+  rc=$?; echo "bench rc=$rc"; tail -c 600 $OUT/bench.log; echo; [ $rc -ne 0 ] && exit $rc
+fi
+for n in $AB; do
+  AB_ALT_LIB=$n=tools/${n}_lab/e-raft_amd/libecorr.so timeout -k 10 300 python -u tools/ab_build.py > $OUT/ab_$n.log 2>&1
+  rc=$?; echo "ab $n rc=$rc"; grep -E "DIFFERENT|differs|median" $OUT/ab_$n.log | tail -4; [ $rc -ne 0 ] && exit $rc
+done
+if [ -n "$ABT" ]; then
+  L=""; for n in $ABT; do L="$L,$n=tools/${n}_lab/e-raft_amd/libecorr.so"; done
+  AB_NOCHECK=1 AB_ALT_LIB=${L#,} timeout -k 10 400 python -u tools/ab_build.py > $OUT/abt.log 2>&1
+  rc=$?; echo "abt rc=$rc"; grep median $OUT/abt.log; [ $rc -ne 0 ] && exit $rc
+fi
+for n in $LK; do
+  AB_ALT_LIB=$n=tools/${n}_lab/e-raft_amd/libecorr.so timeout -k 10 300 python -u tools/ab_lookup.py > $OUT/lk_$n.log 2>&1
+  rc=$?; echo "lk $n rc=$rc"; grep -E "DIFFERENT|differs|median" $OUT/lk_$n.log | tail -8; [ $rc -ne 0 ] && exit $rc
+done
+exit 0

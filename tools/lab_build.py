@@ -513,6 +513,22 @@ COMBOS.update({"noepi16_1cu": ["noepi16", "onecu16"]})
 COMBOS.update({"st16_e16oob": ["st16", "e16oob"], "st16_e16nolds": ["st16", "e16nolds"], "st16_prio_loop": ["st16", "prio_loop"]})
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"], "loopstamps_noepi_mfma16": ["loopstamps", "noepi", "mfma16"]})
 
+# ---- round 4: the split16 epilogue's scaling (bitwise-equal variants unless marked timing only)
+_S16_PK = """                for (int h = 0; h < 2; ++h) {
+                    const floatx2 x = floatx2{acc[qg][tg][2 * h], acc[qg][tg][2 * h + 1]} *
+                                      (sq2 * floatx2{s4[2 * h], s4[2 * h + 1]});
+                    v[tg][2 * h] = MUL ? x[0] : __fdiv_rn(x[0], P.scale);
+                    v[tg][2 * h + 1] = MUL ? x[1] : __fdiv_rn(x[1], P.scale);
+                }"""
+# scalar v_mul_f32 instead of v_pk_mul_f32 (MI355X_MICROARCH.md: packed f32 VALU beside MFMAs is
+# an anti-lever), same products in the same order
+PATCHES["sscale"] = [("build.hip", _S16_PK, """                for (int t = 0; t < 4; ++t) {
+                    const float x = __fmul_rn(acc[qg][tg][t], __fmul_rn(sq, s4[t]));
+                    v[tg][t] = MUL ? x : __fdiv_rn(x, P.scale);
+                }""")]
+# timing only: no scaling at all (v = acc): what the scaling costs
+PATCHES["noscale"] = [("build.hip", _S16_PK, """                for (int t = 0; t < 4; ++t) v[tg][t] = acc[qg][tg][t] + s4[t] * 0.0f;""")]
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
