@@ -142,6 +142,7 @@ def parse():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-next", action="store_true", help="skip the SURVEY §8f next-row measurements")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end ERAFT.forward leg")
     a = ap.parse_args()
     if a.mode == "batch":
         a.batch, a.height, a.width = a.batch or 16, a.height or 60, a.width or 80
@@ -457,6 +458,92 @@ def measure_lookup_fields(blk, B, H, W, iters, look_bytes, device, reps=3):
     return res
 
 
+def measure_e2e(B, iters, device, reps=5):
+    """BASELINE's literal metric, end to end: ERAFT.forward (eraft_amd.network, the reference's
+    module tree and call pattern, eraft.py:88-145) at DSEC 480x640 (15-bin voxel pairs, fmaps
+    D x 60 x 80), batch B, `iters` GRU iterations, warm start (flow_init = a smooth low-res flow),
+    PRNG weights at the reference's init scales (tests/e2e_weights.py; the checkpoints are
+    download-only).  Median of `reps` forwards after a warm-up, outside the headline timed region,
+    for (a) the reference's CorrBlock op sequence on the GPU (bmm, avg_pool2d, grid_sample:
+    oracle/torch_ref.py, a reference leg), (b) eraft_amd.CorrBlock in the reference's call pattern,
+    (c) (b) + the fused lookup/convc1 and the HIP convex upsampling; with the CorrBlock share of
+    each forward (build + iters lookups of that CorrBlock -- for (c) the fused lookup + convc1 --
+    timed alone on the same fmaps)."""
+    import statistics
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import eraft_amd
+    import eraft_amd.network as nw
+    from e2e_weights import make_state_dict
+    from torch_ref import TorchCpuCorrBlock
+    torch.backends.cudnn.benchmark = True
+    g = torch.Generator(device=device).manual_seed(4321)
+    im1 = torch.randn((B, 15, 480, 640), generator=g, device=device)
+    im2 = torch.randn((B, 15, 480, 640), generator=g, device=device)
+    yy, xx = torch.meshgrid(torch.arange(60, device=device, dtype=torch.float32),
+                            torch.arange(80, device=device, dtype=torch.float32), indexing="ij")
+    flow0 = torch.stack([2.0 * torch.sin(yy / 9.0), 1.5 * torch.cos(xx / 11.0)]).expand(B, 2, 60, 80).contiguous()
+    stream = torch.cuda.current_stream(device)
+
+    def net_of(fuse=False, hip_up=False):
+        net = nw.ERAFT({"subtype": "warm_start"}, n_first_channels=15, fuse_motion_corr=fuse, hip_upsample=hip_up)
+        net.load_state_dict(make_state_dict(net.state_dict()))
+        return net.eval().to(device)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return statistics.median(ts)
+
+    res = {"config": f"DSEC 480x640, 15 bins, batch {B}, {iters} iterations, warm start, PRNG weights",
+           "covers": "ERAFT.forward (encoders, CorrBlock, GRU update block, upsampling) between two HIP "
+                     "events, median of %d after a warm-up" % reps}
+    with torch.no_grad():
+        base = net_of()
+        fm1, fm2 = base.fnet([base.image_padder.pad(im1).contiguous(), base.image_padder.pad(im2).contiguous()])
+        fm1, fm2 = fm1.float().contiguous(), fm2.float().contiguous()
+        c1 = eraft_amd.coords_grid(B, 60, 80, device=device) + flow0
+
+        def corr_only(cls, fused):
+            conv = base.update_block.encoder.convc1
+
+            def run():
+                blk = cls(fm1, fm2, num_levels=4, radius=4)
+                for _ in range(iters):
+                    if fused:
+                        blk.lookup_conv1x1_relu(c1, conv.weight, conv.bias)
+                    else:
+                        blk(c1)
+            return run
+        legs = (("reference_corrblock_ops_on_gpu", base, TorchCpuCorrBlock, False),
+                ("eraft_amd_corrblock", base, None, False),
+                ("eraft_amd_corrblock_fused_convc1_hip_upsample", net_of(True, True), None, True))
+        saved = nw.CorrBlock
+        for name, net, cls, fused in legs:
+            try:
+                if cls is not None:
+                    nw.CorrBlock = cls
+                ms = timed(lambda: net(im1, im2, iters=iters, flow_init=flow0))
+            finally:
+                nw.CorrBlock = saved
+            corr_ms = timed(corr_only(cls or eraft_amd.CorrBlock, fused))
+            res[name] = {"ms_per_forward": round(ms, 3), "pairs_per_s": round(B / (ms * 1e-3), 2),
+                         "corrblock_ms": round(corr_ms, 3), "corrblock_share": round(corr_ms / ms, 4)}
+        del fm1, fm2
+    res["speedup_vs_reference_corrblock"] = round(res["reference_corrblock_ops_on_gpu"]["ms_per_forward"] /
+                                                  res["eraft_amd_corrblock"]["ms_per_forward"], 3)
+    torch.cuda.empty_cache()
+    return res
+
+
 def measure_fp32_step(make_block, coords, B, iters, ideal_s, reps=5):
     """North star's literal fp32-MFMA configuration as a whole step (ecorr_build, build_f32_kernel,
     + the 12 lookups), outside the headline timed region: reps steps between two HIP events on the
@@ -614,9 +701,15 @@ def main():
         # own closing event)
         ends = [stages[k + 1][0] for k in range(a.steps - 1)] + [evs[-1][2]]
         look_ms = sum(st[2].elapsed_time(e) for st, e in zip(stages, ends)) / a.steps / iters
+        look_each = [st[2].elapsed_time(e) / iters for st, e in zip(stages, ends)]
+        step_each = [st[0].elapsed_time(e) for st, e in zip(stages, ends)]
     else:
         build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps
         look_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps / iters
+    if not lean:
+        look_each = [e[1].elapsed_time(e[2]) / iters for e in evs]
+        step_each = [e[0].elapsed_time(e[2]) for e in evs]
+    gemm_each = [e[1].elapsed_time(e[2]) for e in stages] if stages else []
     pack_ms = sum(e[0].elapsed_time(e[1]) for e in stages) / len(stages) if stages else 0.0
     gemm_ms = sum(e[1].elapsed_time(e[2]) for e in stages) / len(stages) if stages else build_ms
     for ev in evs + stages:
@@ -667,6 +760,21 @@ def main():
     kernels["lookup"] = {"bound": "hbm", "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(look_gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(look_ms, 4),
                          "launches_per_step": iters, "work_per_launch": f"{look_bytes:.4g} B" + note}
+
+    def spread_seq(xs):   # min / median / max and the first and last of the sequence
+        if not xs:
+            return None
+        ys = sorted(xs)
+        return {"min": round(ys[0], 4), "median": round(ys[len(ys) // 2], 4), "max": round(ys[-1], 4),
+                "first": round(xs[0], 4), "last": round(xs[-1], 4)}
+    # per timed step (this rank): the clock settles over the first ~15 steps of sustained load
+    # (DESIGN.md §5), so the spread shows where in that transient the driver's steps sit
+    kernels["per_step"] = {"steps": a.steps, "step_ms": spread_seq(step_each),
+                           "lookup_ms_per_call": spread_seq(look_each),
+                           "covers": "HIP events of the timed region: a step from its operand pass (or build) "
+                                     "to the next step's; lookup = its 12 calls / 12"}
+    if gemm_each:
+        kernels["build"]["per_step_ms"] = spread_seq(gemm_each)
     if mode == "split" and a.mode == "batch" and world == 1 and not a.no_next:
         with torch.no_grad():
             kernels["build_fp32"] = measure_fp32_build(f1, f2)
@@ -739,6 +847,8 @@ def main():
                                 "forward_interpolate": measure_forward_interpolate(B, H, W, device),
                                 "upsample_flow": measure_upsample(B, H, W, device),
                                 "voxel_grid_dsec": measure_voxel(device)}
+    if a.mode == "batch" and world == 1 and not a.no_next and not a.no_e2e and (H, W) == (60, 80):
+        res["e2e"] = measure_e2e(B, iters, device)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(f1, f2, coords, iters)
     if rank == 0:
