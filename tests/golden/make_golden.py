@@ -17,6 +17,7 @@ reference's OUTPUTS.  What each fixture pins:
   e2e_<case>.npz    ERAFT.forward (eraft.py:88-145) with PRNG weights: final low-res flow and
                     (subsampled) final upsampled flow, standard and warm-start.
   errors.json       shapes on which the reference raises.
+  nonfinite_corr.npz  the pyramid and a lookup from fmaps with +-inf / NaN entries (NONFINITE).
 """
 import hashlib
 import json
@@ -93,6 +94,36 @@ def run_corr_case(name, B, D, H, W, L, r, seed, extra_coords=None):
     np.savez_compressed(os.path.join(HERE, f"corr_{name}.npz"), **{
         k: (np.asarray(v) if not isinstance(v, str) else np.asarray(v)) for k, v in out.items()})
     print(f"corr_{name}: levels {[out[f'level{i}'].shape for i in range(L)]} sets {list(sets)}")
+
+
+# non-finite fmap entries: (tensor, batch, channel, row, col, value); chosen so that the reference's
+# fp32 GEMM (corr.py:58) yields +-inf rows / columns, inf * 0 = NaN, +inf + -inf = NaN and NaN
+NONFINITE = [("f1", 0, 5, 2, 3, np.inf), ("f1", 0, 9, 7, 10, np.nan), ("f2", 0, 17, 4, 14, -np.inf),
+             ("f2", 0, 33, 9, 5, np.inf), ("f1", 0, 33, 11, 1, 0.0), ("f2", 0, 40, 10, 12, np.nan),
+             ("f1", 0, 60, 0, 0, np.inf), ("f2", 0, 60, 1, 1, np.inf), ("f1", 0, 61, 0, 0, np.inf),
+             ("f2", 0, 61, 1, 1, -2.0), ("f1", 1, 7, 8, 15, -np.inf), ("f2", 1, 100, 3, 3, np.inf)]
+
+
+def run_nonfinite():
+    """nonfinite_corr.npz: the pyramid and one lookup from fmaps holding +-inf and NaN entries
+    (fmaps = fmaps(seed) with `entries` [tensor 0/1, b, d, y, x, value] written in)."""
+    B, D, H, W, L, r, seed = 2, 256, 12, 16, 4, 4, 90
+    f1, f2 = fmaps(seed, B, D, H, W)
+    for which, b, d, y, x, v in NONFINITE:
+        (f1 if which == "f1" else f2)[b, d, y, x] = np.float32(v)
+    blk = CorrBlock(torch.from_numpy(f1), torch.from_numpy(f2), num_levels=L, radius=r)
+    ent = np.array([[0 if w == "f1" else 1, b, d, y, x, v] for w, b, d, y, x, v in NONFINITE], dtype=np.float64)
+    out = {"B": B, "D": D, "H": H, "W": W, "L": L, "r": r, "seed": seed, "entries": ent,
+           "sha_fmap1": sha(f1), "sha_fmap2": sha(f2)}
+    for i, lv in enumerate(blk.corr_pyramid):
+        out[f"level{i}"] = lv.numpy()[:, 0].copy()
+    c = prng.coords_with_flow(seed + 100, B, H, W, 3.0)
+    out["coords_s3"] = c
+    out["out_s3"] = blk(torch.from_numpy(c)).numpy()
+    np.savez_compressed(os.path.join(HERE, "nonfinite_corr.npz"), **out)
+    l0 = out["level0"]
+    print(f"nonfinite_corr: level0 +inf {int(np.isposinf(l0).sum())} -inf {int(np.isneginf(l0).sum())} "
+          f"NaN {int(np.isnan(l0).sum())}")
 
 
 def run_large_case(name, B, H, W, seed, n_samples=16384):
@@ -180,6 +211,8 @@ def run_e2e(name, H, W, bins, subtype, seed, warm, up_stride):
 def main():
     if "--e2e-only" in sys.argv:
         return run_all_e2e()
+    if "--nonfinite-only" in sys.argv:
+        return run_nonfinite()
     with open(os.path.join(HERE, "meta.json"), "w") as fh:
         json.dump(META, fh, indent=1)
     run_corr_case("t16x24", 1, 256, 16, 24, 4, 4, 10,
@@ -192,6 +225,7 @@ def main():
     run_corr_case("l1r0_d256", 1, 256, 6, 10, 1, 0, 70)       # single level, radius 0
     run_large_case("dsec60x80", 1, 60, 80, 1000)
     run_large_case("mvsec32x32", 2, 32, 32, 2000)
+    run_nonfinite()
     run_sampler()
     run_errors()
     run_all_e2e()

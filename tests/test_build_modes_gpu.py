@@ -221,3 +221,43 @@ def test_split_two_stage_calls_match_one(ea):
         a = untile(one[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i], i)
         b = untile(two[off[i]:off[i + 1]], B * H * W, h[i], w[i], ntx[i], i)
         assert torch.equal(a, b), f"level {i}"
+
+
+def test_nonfinite_fmap_entries(ea):
+    """fmaps with +-inf and NaN entries against the reference (tests/golden/nonfinite_corr.npz,
+    corr.py:58-60).  fp32 mode (ecorr_build) reproduces the reference's +inf / -inf / NaN pattern
+    exactly.  The split build's documented deviation: every level-0 element whose
+    query or target pixel holds a non-finite entry is NaN (the lo half of an inf is inf - inf), i.e.
+    NaN exactly where the reference is non-finite; every other element finite and normwise within
+    the bar.  Both modes: levels 1-3 bit-exact from their own level 0, non-finite exactly where the
+    reference's are; the lookup non-finite exactly where the reference's is."""
+    from test_oracle_golden import _load, _nonfinite_fmaps, finite_pattern_equal
+    import os
+    from conftest import GOLDEN
+    z = _load(os.path.join(GOLDEN, "nonfinite_corr.npz"))
+    f1n, f2n = _nonfinite_fmaps(z)
+    L, r = int(z["L"]), int(z["r"])
+    ref0 = z["level0"]
+    fin = np.isfinite(ref0)
+    f1, f2 = torch.from_numpy(f1n).to(DEV), torch.from_numpy(f2n).to(DEV)
+    coords = torch.from_numpy(z["coords_s3"]).to(DEV)
+    for mode in ("fp32", "split"):
+        lv = _build(ea, f1, f2, mode, levels=L)
+        if mode == "fp32":
+            assert finite_pattern_equal(lv[0], ref0), "fp32: non-finite pattern"
+        else:
+            assert np.array_equal(np.isnan(lv[0]), ~fin) and np.isfinite(lv[0][fin]).all(), "split: NaN pattern"
+        assert oracle.normwise_err(lv[0][fin], ref0[fin]) <= GEMM_TOL, mode
+        pooled = oracle.pyramid_from_level0(lv[0], L)
+        for i in range(1, L):
+            assert oracle.same_bits(lv[i], pooled[i]), f"{mode}: level {i}"
+            assert np.array_equal(np.isfinite(lv[i]), np.isfinite(z[f"level{i}"])), f"{mode}: level {i} pattern"
+        prev = ea._lib.build_mode()
+        ea._lib.set_build_mode(mode)
+        try:
+            with torch.no_grad():
+                out = ea.CorrBlock(f1, f2, num_levels=L, radius=r)(coords).cpu().numpy()
+        finally:
+            ea._lib.set_build_mode(prev)
+        assert np.array_equal(np.isfinite(out), np.isfinite(z["out_s3"])), f"{mode}: lookup pattern"
+        assert oracle.same_bits(out, oracle.lookup(lv, z["coords_s3"], r)), f"{mode}: lookup vs oracle"

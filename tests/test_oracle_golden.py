@@ -129,3 +129,38 @@ def test_reference_raise_shapes_recorded():
         h, w = map(int, k.split("x"))
         with pytest.raises(RuntimeError):
             oracle.pyramid_from_level0(np.zeros((1, h, w), np.float32), 4)
+
+
+def _nonfinite_fmaps(z):
+    """fmaps of tests/golden/nonfinite_corr.npz: the PRNG fmaps with `entries` written in."""
+    B, D, H, W, seed = (int(z[k]) for k in ("B", "D", "H", "W", "seed"))
+    f1, f2 = prng.normal(seed, (B, D, H, W)), prng.normal(seed + 1, (B, D, H, W))
+    for t, b, d, y, x, v in z["entries"]:
+        (f1 if t == 0 else f2)[int(b), int(d), int(y), int(x)] = np.float32(v)
+    assert _sha(f1) == str(z["sha_fmap1"]) and _sha(f2) == str(z["sha_fmap2"])   # (with the entries)
+    return f1, f2
+
+
+def finite_pattern_equal(got, ref):
+    """Same +inf / -inf / NaN positions (no payload or sign-of-NaN comparison)."""
+    return (np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(np.isposinf(got), np.isposinf(ref))
+            and np.array_equal(np.isneginf(got), np.isneginf(ref)))
+
+
+def test_nonfinite_oracle():
+    """fmaps with +-inf and NaN entries (corr.py:58's fp32 GEMM: +-inf rows / columns, inf * 0 and
+    inf - inf = NaN): the fp64 oracle reproduces the reference's non-finite pattern exactly and its
+    finite values normwise; pooling and the lookup stay bit-exact on the reference's level 0."""
+    z = _load(os.path.join(GOLDEN, "nonfinite_corr.npz"))
+    f1, f2 = _nonfinite_fmaps(z)
+    got = oracle.corr_level0(f1, f2)
+    ref = z["level0"]
+    assert np.isposinf(ref).any() and np.isneginf(ref).any() and np.isnan(ref).any()
+    assert finite_pattern_equal(got, ref)
+    fin = np.isfinite(ref)
+    assert oracle.normwise_err(got[fin], ref[fin]) <= GEMM_TOL
+    L, r = int(z["L"]), int(z["r"])
+    levels = oracle.pyramid_from_level0(ref, L)
+    for i in range(1, L):
+        assert oracle.same_bits(levels[i], z[f"level{i}"]), f"level {i}"
+    assert oracle.same_bits(oracle.lookup([z[f"level{i}"] for i in range(L)], z["coords_s3"], r), z["out_s3"])
