@@ -2,7 +2,8 @@
 # One lab call: optional GPU suite / bench, then A/Bs of lab builds against the tree.
 #   RUN_TESTS=1 RUN_BENCH=1 AB="name1 name2" ABT="timing-only names" LK="lookup lab names" tools/gpu_lab.sh TAG
 # AB: bitwise-checked build A/Bs (each alone vs the tree); ABT: timing-only build A/Bs (no check);
-# LK: lookup A/Bs (tools/ab_lookup.py, bitwise-checked).  Every step under its own time limit,
+# LK: lookup A/Bs (tools/ab_lookup.py, bitwise-checked); STAMPS: build stamps labs (st16*);
+# LKSTAMPS: lookup stamps labs.  Every step under its own time limit,
 # chained: the first failure ends the call.
 cd "$GRAFT_REPO_ROOT"; TAG=${1:-lab}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
 if [ -n "$RUN_TESTS" ]; then
@@ -25,5 +26,15 @@ fi
 for n in $LK; do
   AB_ALT_LIB=$n=tools/${n}_lab/e-raft_amd/libecorr.so timeout -k 10 300 python -u tools/ab_lookup.py > $OUT/lk_$n.log 2>&1
   rc=$?; echo "lk $n rc=$rc"; grep -E "DIFFERENT|differs|median" $OUT/lk_$n.log | tail -8; [ $rc -ne 0 ] && exit $rc
+done
+for n in $STAMPS; do   # build stamps labs (tools/stamps16.py)
+  timeout -k 10 120 python -u tools/stamps16.py tools/${n}_lab/e-raft_amd/libecorr.so > $OUT/stamps_$n.log 2>&1
+  rc=$?; echo "stamps $n rc=$rc"; cat $OUT/stamps_$n.log | tail -7; [ $rc -ne 0 ] && exit $rc
+done
+for n in $LKSTAMPS; do   # lookup stamps (tools/lkstamps.py), smooth and i.i.d. fields
+  for f in smooth iid; do
+    timeout -k 10 120 python -u tools/lkstamps.py tools/${n}_lab/e-raft_amd/libecorr.so $f > $OUT/lkstamps_${n}_$f.log 2>&1
+    rc=$?; echo "lkstamps $n $f rc=$rc"; cat $OUT/lkstamps_${n}_$f.log | tail -12; [ $rc -ne 0 ] && exit $rc
+  done
 done
 exit 0

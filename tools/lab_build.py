@@ -512,6 +512,7 @@ COMBOS.update({"dmaqoob": ["dmaoob", "qoob"], "noepi_r2": ["noepi"]})
 COMBOS.update({"noepi16_1cu": ["noepi16", "onecu16"]})
 COMBOS.update({"st16_e16oob": ["st16", "e16oob"], "st16_e16nolds": ["st16", "e16nolds"], "st16_prio_loop": ["st16", "prio_loop"]})
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"], "loopstamps_noepi_mfma16": ["loopstamps", "noepi", "mfma16"]})
+COMBOS.update({"st16_sscale": ["st16", "sscale"], "st16_noscale": ["st16", "noscale"]})
 
 # ---- round 4: the split16 epilogue's scaling (bitwise-equal variants unless marked timing only)
 _S16_PK = """                for (int h = 0; h < 2; ++h) {
@@ -528,6 +529,50 @@ PATCHES["sscale"] = [("build.hip", _S16_PK, """                for (int t = 0; t
                 }""")]
 # timing only: no scaling at all (v = acc): what the scaling costs
 PATCHES["noscale"] = [("build.hip", _S16_PK, """                for (int t = 0; t < 4; ++t) v[tg][t] = acc[qg][tg][t] + s4[t] * 0.0f;""")]
+
+# ---- round 4: per-workgroup timeline of the lookup (lookup_cols_reg): s_memrealtime stamps at the
+# start, after the origin barrier, after the staging barrier, and each wave's end after its own
+# stores retired (vmcnt(0)); + HW_ID / XCC_ID.  Timing diagnosis only (tools/lkstamps.py).
+LK_DECL = """
+__device__ unsigned long long g_lk[262144][8];
+"""
+LK_EXPORT = """
+extern "C" __attribute__((visibility("default"))) int ecorr_lab_lkstamps(void* dst, int n) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ecorr::g_lk), (size_t)n * 64, 0, hipMemcpyDeviceToHost);
+}
+"""
+PATCHES["lkstamps"] = [
+    ("lookup.hip", "constexpr int NT = 256;   // threads of the generic kernels", "constexpr int NT = 256;   // threads of the generic kernels" + LK_DECL),
+    ("lookup.hip", """    __shared__ WB st;
+    const int tid = threadIdx.x, g = tid % QB;""", """    __shared__ WB st;
+    const unsigned long long lk_t0 = __builtin_amdgcn_s_memrealtime();
+    const int lk_id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int tid = threadIdx.x, g = tid % QB;"""),
+    ("lookup.hip", """    __syncthreads();
+    stage_windows<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid);
+""", """    __syncthreads();
+    const unsigned long long lk_t1 = __builtin_amdgcn_s_memrealtime();
+    stage_windows<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid);
+    const unsigned long long lk_t2 = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && lk_id < 262144) {
+        g_lk[lk_id][0] = lk_t0;
+        g_lk[lk_id][1] = lk_t1;
+        g_lk[lk_id][2] = lk_t2;
+        g_lk[lk_id][6] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+        g_lk[lk_id][7] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+    }
+"""),
+    ("lookup.hip", """                                                      sbase + ((part * AP + ai) * K + bb) * P.q_count * 4, 2);
+            }
+    }
+}""", """                                                      sbase + ((part * AP + ai) * K + bb) * P.q_count * 4, 2);
+            }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    if (g == 0 && lk_id < 262144) g_lk[lk_id][3 + part] = __builtin_amdgcn_s_memrealtime();
+}"""),
+    ("lookup.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + LK_EXPORT),
+]
 
 
 def build(name):
