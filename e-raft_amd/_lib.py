@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -49,6 +49,10 @@ SYMBOLS = {
     "ecorr_lookup": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),
     # (pyramid, coords, B, H, W, q_count, levels, radius, weight[O][C], bias, O, out, stream)
     "ecorr_lookup_conv1x1_relu": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _p, _p]),
+    # (O, C, floats*) / (weight[O][C], O, C, packed, stream) / as ecorr_lookup_conv1x1_relu, packed weight
+    "ecorr_conv1x1_packed_size": (_i, [_i, _i, ctypes.POINTER(_i64)]),
+    "ecorr_conv1x1_pack": (_i, [_p, _i, _i, _p, _p]),
+    "ecorr_lookup_conv1x1_relu_packed": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _p, _p]),
     "ecorr_bilinear_sampler": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _p]),
     "ecorr_coords_grid": (_i, [_i, _i, _i, _p, _p]),
     # (chunks, chunk, world, B, C, H, W, out, stream)
@@ -206,3 +210,34 @@ def build_pyramid(fmap1, fmap2, B, D, H, W, q_count, levels, off, what, mode=Non
         check(lib().ecorr_build(fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, q_count, levels,
                                 pyr.data_ptr(), st), what)
     return pyr
+
+
+# Packed convc1 weights (ecorr_conv1x1_pack) per weight tensor: id -> (weakref, version, O, C, packed).
+# The fused lookup + convc1 kernel reads the weight in its MFMA fragment order; ERAFT.forward calls
+# it `iters` times per forward with the same convc1.weight, so the weight is re-laid once and again
+# only after an in-place update (the tensor's version counter) -- or on every call for tensors
+# without a version counter (inference-mode tensors).
+_packed_weights = {}
+
+
+def packed_conv1x1_weight(weight, O, C):
+    import weakref
+    try:
+        version = weight._version
+    except RuntimeError:   # inference tensor: no version counter, no caching
+        version = None
+    key = id(weight)
+    ent = _packed_weights.get(key)
+    if (version is not None and ent is not None and ent[0]() is weight and ent[1] == version
+            and ent[2:4] == (O, C) and ent[4].device == weight.device):
+        return ent[4]
+    wt = weight.reshape(O, C).contiguous()
+    n = ctypes.c_int64()
+    check(lib().ecorr_conv1x1_packed_size(O, C, ctypes.byref(n)), "convc1 weight pack")
+    packed = torch.empty(n.value, dtype=torch.float32, device=weight.device)
+    check(lib().ecorr_conv1x1_pack(wt.data_ptr(), O, C, packed.data_ptr(), stream_of(weight)), "convc1 weight pack")
+    if version is not None:
+        for k in [k for k, e in _packed_weights.items() if e[0]() is None]:
+            del _packed_weights[k]
+        _packed_weights[key] = (weakref.ref(weight), version, O, C, packed)
+    return packed

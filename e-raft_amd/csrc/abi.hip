@@ -216,7 +216,28 @@ ECORR_EXPORT int ecorr_lookup_conv1x1_relu(const float* pyramid, const float* co
     LookupParams P{};
     const int st = lookup_params(pyramid, coords, B, H, W, q_count, levels, radius, out, &P);
     if (st != ECORR_OK) return st;
-    return launch_lookup_conv(P, B, weight, bias, O, out, (hipStream_t)stream);
+    return launch_lookup_conv(P, B, weight, bias, O, out, (hipStream_t)stream, false);
+}
+
+ECORR_EXPORT int ecorr_conv1x1_packed_size(int O, int C, int64_t* floats) {
+    if (!floats || O <= 0 || O % 64 != 0 || C <= 0) return ECORR_EINVAL;
+    *floats = conv1x1_packed_floats(O, C);
+    return ECORR_OK;
+}
+
+ECORR_EXPORT int ecorr_conv1x1_pack(const float* weight, int O, int C, float* packed, void* stream) {
+    if (!weight || !packed) return ECORR_EINVAL;
+    return launch_conv1x1_pack(weight, O, C, packed, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_lookup_conv1x1_relu_packed(const float* pyramid, const float* coords, int B, int H, int W,
+                                                  int q_count, int levels, int radius, const float* packed,
+                                                  const float* bias, int O, float* out, void* stream) {
+    if (!packed) return ECORR_EINVAL;
+    LookupParams P{};
+    const int st = lookup_params(pyramid, coords, B, H, W, q_count, levels, radius, out, &P);
+    if (st != ECORR_OK) return st;
+    return launch_lookup_conv(P, B, packed, bias, O, out, (hipStream_t)stream, true);
 }
 
 ECORR_EXPORT int ecorr_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,

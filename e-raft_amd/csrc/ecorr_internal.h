@@ -68,7 +68,9 @@ struct LookupParams {
 int launch_lookup(const LookupParams& P, int B, hipStream_t stream);
 
 int launch_lookup_conv(const LookupParams& P, int B, const float* wt, const float* bias, int O, float* out,
-                       hipStream_t stream);
+                       hipStream_t stream, bool packed);
+int64_t conv1x1_packed_floats(int O, int C);
+int launch_conv1x1_pack(const float* wt, int O, int C, float* packed, hipStream_t stream);
 
 int launch_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,
                             int Hg, int Wg, float* out, float* mask, hipStream_t stream);

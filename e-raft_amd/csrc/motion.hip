@@ -11,10 +11,12 @@
 //   lookup  for each level: stage_level (lookup_stage.h) then blend the level's (2r+1)^2 samples
 //           of every query into the LDS tile T[c][q] (c-major, 41.5 KB at C = 324);
 //   GEMM    wave w computes output channels [64w, 64w + 64) x the 32 queries as two
-//           v_mfma_f32_32x32x2_f32 tiles over K = C: A = W^T[c][o] staged through LDS in 16-
-//           channel chunks (float4 register loads one chunk ahead, double-buffered; the 331 KB
-//           weight is shared by every workgroup, so it streams from L2), B = T from LDS; bias +
-//           ReLU in the epilogue, stores coalesced along the queries.
+//           v_mfma_f32_32x32x2_f32 tiles over K = C: A = W[o][c] fragments loaded per lane in
+//           16-channel chunks (float4 register loads one chunk ahead; the 331 KB weight is shared
+//           by every workgroup, so it streams from L2) -- from the packed weight (ecorr_conv1x1_pack:
+//           fragment order, one contiguous 1-KB piece per wave load) or from the conv weight as
+//           stored (64 rows' 16-byte pieces per load) -- B = T from LDS; bias + ReLU in the
+//           epilogue, stores coalesced along the queries.
 // The GEMM is MFMA-bound (2 * O * C flops per query), the lookup HBM-bound; 76 KB of LDS (the
 // weight chunks alias the dead window stage) lets two workgroups share a CU so one's gather
 // overlaps the other's MFMAs.
@@ -26,6 +28,8 @@
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
 #include "lookup_stage.h"
+
+#include <algorithm>
 
 namespace ecorr {
 
@@ -40,9 +44,34 @@ constexpr int KC = 16;     // channels per weight chunk
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// The weight in the GEMM's A-fragment order (pack_weight_kernel, ecorr_conv1x1_pack): for output
+// block ob64 (64 channels = one wave's two 32x32 tiles), channel chunk kc (16 channels) and piece p
+// (tile p >> 1, half p & 1), lane l holds W[64 ob64 + 32 (p >> 1) + (l & 31)][16 kc + 8 (l >> 5) +
+// 4 (p & 1) + e], e = 0..3 (zeros past O or C), 16 bytes at ((ob64 nkc + kc) 4 + p) 1 KB + 16 l: each
+// wave load is one contiguous 1-KB piece (8 whole lines) instead of 64 rows' 16-byte pieces.
+__host__ __device__ constexpr int packed_chunks(int C) { return (C + KC - 1) / KC; }
+
+__global__ __launch_bounds__(NTM) void pack_weight_kernel(const float* __restrict__ wt, int O, int C,
+                                                          float* __restrict__ packed) {
+    const int nkc = packed_chunks(C);
+    const int64_t n = (int64_t)(O / OW) * nkc * 4 * 64;   // 16-byte pieces
+    for (int64_t i = blockIdx.x * (int64_t)NTM + threadIdx.x; i < n; i += (int64_t)gridDim.x * NTM) {
+        const int l = (int)(i & 63), p = (int)((i >> 6) & 3);
+        const int64_t r = i >> 8;
+        const int kc = (int)(r % nkc), ob = (int)(r / nkc);
+        const int o = ob * OW + 32 * (p >> 1) + (l & 31);
+        const int c = kc * KC + 8 * (l >> 5) + 4 * (p & 1);
+        floatx4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (o < O && c + e < C) ? wt[(int64_t)o * C + c + e] : 0.0f;
+        reinterpret_cast<floatx4*>(packed)[i] = v;
+    }
+}
+
 // PAIR (every level width even): windows staged as 8-byte column pairs (lookup_stage.h).
-template <int R, bool PAIR>
-__global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, const float* __restrict__ wt /* [O][C] */,
+// PACKED: wt is the packed weight above; else the conv weight [O][C] as stored.
+template <int R, bool PAIR, bool PACKED>
+__global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, const float* __restrict__ wt,
                                                              const float* __restrict__ bias, int O,
                                                              float* __restrict__ out) {
     using WS = WindowStage<R, QBM, PAIR>;
@@ -99,15 +128,24 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
     // sums the channels in a fixed permuted order -- still an exact fmaf chain per output.)
     const int kr = lane >> 5, col = lane & 31;
     const int nkc = CPAD / KC;
+    const int pnkc = packed_chunks(C);   // PACKED: chunks of the packed weight (later ones read 0)
     __syncthreads();   // T complete
-    const __amdgpu_buffer_rsrc_t wsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wt), 0, (int)((int64_t)O * C * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(wt), 0, PACKED ? (int)((int64_t)(O / OW) * pnkc * 4096) : (int)((int64_t)O * C * 4), 0x00020000);
     for (int oc = 0; oc < O; oc += OB) {
         const int ob = oc + wave * OW;   // this wave's first output channel
         // W row o starts at o * C floats; rows beyond O and channels beyond C read 0 (range check)
         const int r0 = (ob + col) * C, r1 = (ob + 32 + col) * C;
         floatx4 wc[4], wn[4];   // [tile][half]: tile i, channels c0 + 8 kr + 4 h .. +3
         auto load_w = [&](floatx4 (&w)[4], int c0) {
+            if constexpr (PACKED) {   // one 1-KB piece per load; the block / chunk / piece offset is wave-uniform
+                const int kc = c0 / KC;
+                const int base = kc < pnkc ? (((ob / OW) * pnkc + kc) * 4) * 1024 : 0x7ffff000;
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+                    w[p] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(wsrc, lane * 16, base + p * 1024, 0));
+                return;
+            }
             const int c = c0 + 8 * kr;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -160,16 +198,33 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
 
 }  // namespace
 
+int64_t conv1x1_packed_floats(int O, int C) { return (int64_t)(O / OW) * packed_chunks(C) * 4 * 64 * 4; }
+
+int launch_conv1x1_pack(const float* wt, int O, int C, float* packed, hipStream_t stream) {
+    if (O <= 0 || O % OW != 0 || C <= 0) return ECORR_EINVAL;
+    const int64_t n = conv1x1_packed_floats(O, C) / 4;
+    const unsigned grid = (unsigned)std::min<int64_t>((n + NTM - 1) / NTM, 4096);
+    hipLaunchKernelGGL(pack_weight_kernel, dim3(grid), dim3(NTM), 0, stream, wt, O, C, packed);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
+}
+
 int launch_lookup_conv(const LookupParams& P, int B, const float* wt, const float* bias, int O, float* out,
-                       hipStream_t stream) {
+                       hipStream_t stream, bool packed) {
     if (P.radius != 4) return ECORR_ERADIUS;
     if (P.levels > 4) return ECORR_ELEVELS;
     if (O <= 0 || O % OW != 0) return ECORR_EINVAL;
+    if (packed && conv1x1_packed_floats(O, P.C) * 4 >= 0x7fffffffLL) return ECORR_EINVAL;
     const dim3 grid((unsigned)((P.q_count + QBM - 1) / QBM), (unsigned)B), block(NTM);
     bool pair = true;   // column-pair staging: every level width even, 8-byte aligned levels
     for (int lv = 0; lv < P.levels; ++lv) pair &= P.lw[lv] % 2 == 0 && (uintptr_t)P.lvl[lv] % 8 == 0;
-    if (pair) hipLaunchKernelGGL((lookup_conv_kernel<4, true>), grid, block, 0, stream, P, wt, bias, O, out);
-    else hipLaunchKernelGGL((lookup_conv_kernel<4, false>), grid, block, 0, stream, P, wt, bias, O, out);
+    if (packed) {
+        if (pair) hipLaunchKernelGGL((lookup_conv_kernel<4, true, true>), grid, block, 0, stream, P, wt, bias, O, out);
+        else hipLaunchKernelGGL((lookup_conv_kernel<4, false, true>), grid, block, 0, stream, P, wt, bias, O, out);
+    } else {
+        if (pair) hipLaunchKernelGGL((lookup_conv_kernel<4, true, false>), grid, block, 0, stream, P, wt, bias, O, out);
+        else hipLaunchKernelGGL((lookup_conv_kernel<4, false, false>), grid, block, 0, stream, P, wt, bias, O, out);
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
 }

@@ -259,13 +259,15 @@ class RowShardedCorrBlock:
             if bias.numel() != O:
                 raise RuntimeError(f"bias has {bias.numel()} elements, expected {O}")
             bias = bias.contiguous()
-        wt = weight.reshape(O, C).contiguous()
+        if O <= 0 or O % 64 != 0:
+            raise RuntimeError(f"{O} output channels: the fused kernel needs a positive multiple of 64")
         if self.world == 1:
             out = torch.empty((B, O, H, W), dtype=torch.float32, device=self._device)
         else:
             out = self._ex.send_slab(B, O, W, device=self._device)
         with _lib.on_device(self._device):
-            _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu(
+            wt = _lib.packed_conv1x1_weight(weight, O, C)   # MFMA fragment order, re-laid once per weight
+            _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu_packed(
                 self._pyramid.data_ptr(), coords_rows.data_ptr(), B, H, W, self.q_count, self.num_levels,
                 self.radius, wt.data_ptr(), None if bias is None else bias.data_ptr(), O, out.data_ptr(),
                 _lib.stream_of(out)), "RowShardedCorrBlock lookup+conv1x1+relu")

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 13
+#define ECORR_ABI_VERSION 14
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -116,6 +116,19 @@ int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W,
 int ecorr_lookup_conv1x1_relu(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
                               int levels, int radius, const float* weight, const float* bias, int O,
                               float* out, void* stream);
+
+/* The same with the weight re-laid once in the fused kernel's MFMA fragment order (ABI 14): each
+ * wave load of the weight stream is then one contiguous 1-KB piece.  ecorr_conv1x1_packed_size
+ * gives the packed float count for O output and C = levels*(2r+1)^2 input channels (O a positive
+ * multiple of 64); ecorr_conv1x1_pack writes it from weight float[O][C] (stream-ordered);
+ * ecorr_lookup_conv1x1_relu_packed takes it in place of the weight -- bitwise the same result as
+ * ecorr_lookup_conv1x1_relu with that weight.  The packed weight stays valid until the weight
+ * changes (the Python binding re-packs on every in-place update of the weight tensor). */
+int ecorr_conv1x1_packed_size(int O, int C, int64_t* floats);
+int ecorr_conv1x1_pack(const float* weight, int O, int C, float* packed, void* stream);
+int ecorr_lookup_conv1x1_relu_packed(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
+                                     int levels, int radius, const float* packed, const float* bias, int O,
+                                     float* out, void* stream);
 
 /* Generic bilinear_sampler: img float[N][C][h][w], coords float[N][Hg][Wg][2] in pixels ->
  * out float[N][C][Hg][Wg]; mask (nullable) float[N][Hg][Wg] = 1 where the normalized sample

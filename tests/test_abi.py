@@ -109,6 +109,16 @@ def test_argument_validation_before_launch(ea):
     assert F(8, 8, 1, 64, 64, 4096, 5, 4, 8, None, 64, 8, None) == _lib.ECORR_ELEVELS   # levels > 4
     assert F(8, 8, 1, 16, 16, 256, 4, 4, 8, None, 96, 8, None) == _lib.ECORR_EINVAL
     assert F(8, 8, 1, 16, 16, 256, 4, 4, None, None, 64, 8, None) == _lib.ECORR_EINVAL
+    Fp = L.ecorr_lookup_conv1x1_relu_packed   # ... with the packed weight (ABI 14)
+    assert Fp(8, 8, 1, 16, 16, 256, 4, 3, 8, None, 64, 8, None) == _lib.ECORR_ERADIUS
+    assert Fp(8, 8, 1, 16, 16, 256, 4, 4, 8, None, 96, 8, None) == _lib.ECORR_EINVAL
+    assert Fp(8, 8, 1, 16, 16, 256, 4, 4, None, None, 64, 8, None) == _lib.ECORR_EINVAL
+    n = ctypes.c_int64()
+    assert L.ecorr_conv1x1_packed_size(256, 324, ctypes.byref(n)) == _lib.ECORR_OK
+    assert n.value == 4 * 21 * 4 * 64 * 4   # [O / 64][ceil(C / 16)][4 pieces][64 lanes][4 floats]
+    assert L.ecorr_conv1x1_packed_size(96, 324, ctypes.byref(n)) == _lib.ECORR_EINVAL
+    assert L.ecorr_conv1x1_pack(None, 256, 324, 8, None) == _lib.ECORR_EINVAL
+    assert L.ecorr_conv1x1_pack(8, 100, 324, 8, None) == _lib.ECORR_EINVAL
     # the split build's stages validate like the whole call (no workspace / no operands)
     assert L.ecorr_build_split_pack(8, 8, 1, 256, 8, 8, 64, None, None) == _lib.ECORR_EINVAL
     assert L.ecorr_build_split_pack(None, 8, 1, 256, 8, 8, 64, 256, None) == _lib.ECORR_EINVAL

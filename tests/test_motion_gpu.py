@@ -93,3 +93,31 @@ def test_fused_rejects_unsupported(ea):
         blk = ea.CorrBlock(torch.zeros(1, 8, 16, 16, device=DEV), torch.zeros(1, 8, 16, 16, device=DEV))
         with pytest.raises(RuntimeError):   # weight does not map 324 channels
             blk.lookup_conv1x1_relu(torch.zeros(1, 2, 16, 16, device=DEV), torch.zeros(64, 300, device=DEV))
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 16, 24, 4, 256), (1, 32, 23, 40, 3, 128)], ids=["l4_o256", "l3_o128"])
+def test_packed_weight_matches_weight_as_stored(ea, shape):
+    """ecorr_lookup_conv1x1_relu_packed (the weight in MFMA fragment order, what CorrBlock uses) is
+    bitwise ecorr_lookup_conv1x1_relu with the weight as stored; an in-place weight update re-packs."""
+    from eraft_amd import _lib
+    B, D, H, W, L, O = shape
+    C = L * 81
+    with torch.no_grad():
+        blk = _block(ea, B, D, H, W, 51, L)
+        coords = torch.from_numpy(prng.coords_with_flow(52, B, H, W, 3.0)).to(DEV)
+        wgt = torch.from_numpy(prng.normal(53, (O, C, 1, 1)) * 0.05).to(DEV)
+        bias = torch.from_numpy(prng.normal(54, (O,)) * 0.1).to(DEV)
+        got = blk.lookup_conv1x1_relu(coords, wgt, bias)
+        ref = torch.empty_like(got)
+        _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu(
+            blk._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, L, 4, wgt.data_ptr(), bias.data_ptr(), O,
+            ref.data_ptr(), _lib.stream_of(coords)), "unpacked")
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
+        wgt.mul_(-1.0)   # in place: the cached packed weight must not be reused
+        got2 = blk.lookup_conv1x1_relu(coords, wgt, bias)
+        _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu(
+            blk._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, L, 4, wgt.data_ptr(), bias.data_ptr(), O,
+            ref.data_ptr(), _lib.stream_of(coords)), "unpacked")
+        torch.cuda.synchronize()
+        assert torch.equal(got2, ref) and not torch.equal(got2, got)
