@@ -139,11 +139,15 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
         floatx4 wc[4], wn[4];   // [tile][half]: tile i, channels c0 + 8 kr + 4 h .. +3
         auto load_w = [&](floatx4 (&w)[4], int c0) {
             if constexpr (PACKED) {   // one 1-KB piece per load; the block / chunk / piece offset is wave-uniform
+                // chunks past the packed ones (rows of the padded tile beyond C) read 0: the
+                // out-of-range offset goes in the voffset, which the range check covers
                 const int kc = c0 / KC;
-                const int base = kc < pnkc ? (((ob / OW) * pnkc + kc) * 4) * 1024 : 0x7ffff000;
+                const bool in = kc < pnkc;
+                const int base = in ? (((ob / OW) * pnkc + kc) * 4) * 1024 : 0;
 #pragma unroll
                 for (int p = 0; p < 4; ++p)
-                    w[p] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(wsrc, lane * 16, base + p * 1024, 0));
+                    w[p] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                           wsrc, in ? lane * 16 : 0x7ffff000, base + p * 1024, 0));
                 return;
             }
             const int c = c0 + 8 * kr;
