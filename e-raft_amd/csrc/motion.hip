@@ -143,7 +143,7 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
                 // out-of-range offset goes in the voffset, which the range check covers
                 const int kc = c0 / KC;
                 const bool in = kc < pnkc;
-                const int base = in ? (((ob / OW) * pnkc + kc) * 4) * 1024 : 0;
+                const int base = __builtin_amdgcn_readfirstlane(in ? (((ob / OW) * pnkc + kc) * 4) * 1024 : 0);
 #pragma unroll
                 for (int p = 0; p < 4; ++p)
                     w[p] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -168,7 +168,8 @@ __global__ __launch_bounds__(NTM, 2) void lookup_conv_kernel(LookupParams P, con
 #pragma unroll
         for (int r = 0; r < 16; ++r) { acc0[r] = 0.0f; acc1[r] = 0.0f; }
         load_w(wc, 0);
-        for (int kc = 0; kc < nkc; ++kc) {
+#pragma unroll 1
+        for (int kc = 0; kc < nkc; ++kc) {   // rolled (unrolled, even by two, it spills: 256 VGPRs + scratch)
             if (kc + 1 < nkc) load_w(wn, (kc + 1) * KC);
             float bq[8];
 #pragma unroll
