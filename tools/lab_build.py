@@ -574,6 +574,53 @@ PATCHES["lkstamps"] = [
     ("lookup.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + LK_EXPORT),
 ]
 
+# ---- round 4: lookup with only the window end-point chains before the staging loads; the other
+# chains (7 y, 3 x per thread) computed while those loads are in flight (bitwise the same)
+PATCHES["lk_late"] = [("lookup.hip", """    float fy[K], wy[K], fx[AP], wx[AP], x0 = 0.0f, xl = 0.0f;
+    if (valid) {
+        const int64_t Q = P.q_count;
+        const float inv = 1.0f / (float)(1 << lv);  // coords / 2**i is an exact scaling
+        const float cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
+        const float cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);
+        const float wm1 = (float)(P.lw[lv] - 1), hm1 = (float)(P.lh[lv] - 1);
+#pragma unroll
+        for (int bb = 0; bb < K; ++bb) coord_chain<R>(cy, bb, hm1, fy[bb], wy[bb]);
+#pragma unroll
+        for (int ai = 0; ai < AP; ++ai) coord_chain<R>(cx, part * AP + ai, wm1, fx[ai], wx[ai]);
+        float dummy;
+        coord_chain<R>(cx, 0, wm1, x0, dummy);
+        coord_chain<R>(cx, K - 1, wm1, xl, dummy);
+    }""", """    float fy[K], wy[K], fx[AP], wx[AP], x0 = 0.0f, xl = 0.0f;
+    float cx = 0.0f, cy = 0.0f;
+    const float wm1 = (float)(P.lw[lv] - 1), hm1 = (float)(P.lh[lv] - 1);
+    if (valid) {
+        const int64_t Q = P.q_count;
+        const float inv = 1.0f / (float)(1 << lv);  // coords / 2**i is an exact scaling
+        cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
+        cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);
+        coord_chain<R>(cy, 0, hm1, fy[0], wy[0]);
+        coord_chain<R>(cy, K - 1, hm1, fy[K - 1], wy[K - 1]);
+        float dummy;
+        coord_chain<R>(cx, 0, wm1, x0, dummy);
+        coord_chain<R>(cx, K - 1, wm1, xl, dummy);
+    }"""),
+    ("lookup.hip", """    __syncthreads();
+    stage_windows<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid);
+""", """    __syncthreads();
+    {
+        StageRegs<R, QB, NTQ, PAIR> sr;
+        stage_issue<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid, sr);
+        if (valid) {   // the remaining chains under the staging loads' latency
+#pragma unroll
+            for (int bb = 1; bb < K - 1; ++bb) coord_chain<R>(cy, bb, hm1, fy[bb], wy[bb]);
+#pragma unroll
+            for (int ai = 0; ai < AP; ++ai) coord_chain<R>(cx, part * AP + ai, wm1, fx[ai], wx[ai]);
+        }
+        stage_commit<R, QB, NTQ, PAIR>(st, sr);
+        __syncthreads();
+    }
+""")]
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
