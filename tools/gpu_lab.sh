@@ -6,6 +6,9 @@
 # LKSTAMPS: lookup stamps labs.  Every step under its own time limit,
 # chained: the first failure ends the call.
 cd "$GRAFT_REPO_ROOT"; TAG=${1:-lab}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+if [ -n "$LISTCTR" ]; then   # the PMC counters this box offers
+  timeout -k 10 60 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "counters rc=$?"
+fi
 if [ -n "$RUN_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; grep -E 'FAILED|ERROR|passed|failed' $OUT/pytest_gpu.log | tail -5; [ $rc -ne 0 ] && exit $rc

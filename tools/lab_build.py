@@ -621,6 +621,113 @@ PATCHES["lk_late"] = [("lookup.hip", """    float fy[K], wy[K], fx[AP], wx[AP], 
     }
 """)]
 
+# ---- round 4: lookup staging with lanes = (query, column pair, row group): a task is one column
+# pair of one query's window at rows rg, rg + 4, rg + 8 (rg = lane & 3), so the 64 lanes of a load
+# instruction cover 16 (query, pair) items x 4 consecutive rows -- about 9-10 distinct 128-B lines
+# per instruction instead of ~21 (one row of ~11 queries' windows) -- and every row step is one
+# constant offset (+4 rows: one tile row / two or four block rows).  Bitwise the same.
+LK_RG_FN = """
+// lab: task-per-(query, pair, row group) staging, PAIR only (see tools/lab_build.py lk_rg)
+template <int R, int QB, int NTQ>
+struct StageRegsRG {
+    static constexpr int S = 2 * R + 3, NPX = (S + 1) / 2, TASKS = QB * NPX * 4;
+    static constexpr int NT = (TASKS + NTQ - 1) / NTQ, NR = (S + 3) / 4;
+    float vals[NT][NR][2];
+    int dst[NT];    // LDS slot of row rg of the task's pair (-1: no task)
+    int skip[NT];   // the pair half (0 / 1) outside the S-slot row, else -1
+};
+
+template <int R, int QB, int NTQ>
+__device__ __forceinline__ void stage_issue_rg(const WindowBuf<R, QB, true>& st, const LookupParams& P, int lv, int b,
+                                               int q0, int tid, StageRegsRG<R, QB, NTQ>& sr) {
+    using WS = WindowBuf<R, QB, true>;
+    using SR = StageRegsRG<R, QB, NTQ>;
+    constexpr int S = WS::S, SP = WS::SP, SW = WS::SW, NPX = SR::NPX;
+    static_assert(NTQ % 4 == 0 && (NTQ / 4) % NPX == 0, "rg and pair fixed per thread");
+    const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
+    const int64_t hw = P.lsz[lv];
+    const int64_t R0 = (int64_t)b * P.q_count + q0;
+    const int64_t g0 = R0 >> 6;
+    const float* __restrict__ lvbase = P.lvl[lv] + (ntx < 0 ? g0 * kGroup * hw : R0 * hw);
+    const int nq = min(QB, P.q_count - q0);
+    const int64_t span = ntx < 0 ? (((R0 + nq - 1) >> 6) - g0 + 1) * kGroup * hw : nq * hw;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lvbase), 0, (int)(span * 4), 0x00020000);
+    const bool tiled = ntx > 0, ilv = ntx < 0;
+    const int sy = ilv ? ilv_sy(lv) : 2, sx = ilv ? ilv_sx(lv) : 3;
+    const int ymask = tiled || ilv ? (1 << sy) - 1 : 0;
+    const int step4 = tiled ? 128 * ntx : ilv ? (4 >> sy) * -ntx * kGroup * (1 << (sy + sx)) * 4 : 16 * w;
+    constexpr int OOB = 0x7ffffff0;
+    const int rg = tid & 3, px = (tid >> 2) % NPX, gq0 = (tid >> 2) / NPX;
+    constexpr int DQ = NTQ / 4 / NPX;   // queries between a thread's tasks
+#pragma unroll
+    for (int c = 0; c < SR::NT; ++c) {
+        const int gq = gq0 + DQ * c;
+        const bool live = gq < QB;
+        const int gqs = live ? gq : 0;
+        const int xo = st.org[gqs][0], y0 = st.org[gqs][1], info = st.org[gqs][2];
+        const int odd = xo & 1;
+        const int x = xo - odd + 2 * px;
+        const int ny = (info >> 16) & 0xff;
+        const bool colin = live && (info & 0xff) == 0 && 2 * px < ((info >> 8) & 0xff) + odd && (unsigned)x < (unsigned)w;
+        sr.dst[c] = live ? WS::W0 + gq * SP + rg * SW + 2 * px - odd : -1;
+        sr.skip[c] = odd && px == 0 ? 0 : !odd && 2 * px == S - 1 ? 1 : -1;
+        const int rlo = max(0, -y0), rhi = colin ? max(rlo, min(ny, h - y0)) : rlo;
+        const int y = y0 + rg;
+        int off;
+        if (tiled) {
+            off = (int)(gqs * hw) * 4 + ((((y >> 2) * ntx + (x >> 3)) << 5) + ((y & 3) << 3) + (x & 7)) * 4;
+        } else if (ilv) {
+            const int64_t Rq = R0 + gqs;
+            off = (int)((((Rq >> 6) - g0) * kGroup * hw +
+                         ((int64_t)((y >> sy) * -ntx + (x >> sx)) * kGroup + (Rq & (kGroup - 1))) * (1 << (sy + sx)) +
+                         ((y & ymask) << sx) + (x & ((1 << sx) - 1))) * 4);
+        } else {
+            off = (int)(gqs * hw) * 4 + (y * w + x) * 4;
+        }
+#pragma unroll
+        for (int j = 0; j < SR::NR; ++j) {
+            const int ry = rg + 4 * j;
+            const bool need = ry < S && (unsigned)(ry - rlo) < (unsigned)(rhi - rlo);
+            const uint2v u = __builtin_amdgcn_raw_buffer_load_b64(rsrc, need ? off : OOB, 0, 0);
+            sr.vals[c][j][0] = __uint_as_float(u.x);
+            sr.vals[c][j][1] = __uint_as_float(u.y);
+            off += step4;
+        }
+    }
+}
+
+template <int R, int QB, int NTQ>
+__device__ __forceinline__ void stage_commit_rg(WindowBuf<R, QB, true>& st, const StageRegsRG<R, QB, NTQ>& sr, int tid) {
+    using SR = StageRegsRG<R, QB, NTQ>;
+    constexpr int SW = WindowBuf<R, QB, true>::SW, DUMMY = WindowBuf<R, QB, true>::DUMMY, S = SR::S;
+    const int rg = tid & 3;
+#pragma unroll
+    for (int c = 0; c < SR::NT; ++c)
+        if (sr.dst[c] >= 0)
+#pragma unroll
+            for (int j = 0; j < SR::NR; ++j)
+                if (rg + 4 * j < S)
+#pragma unroll
+                    for (int v = 0; v < 2; ++v)
+                        st.win[sr.skip[c] == v ? DUMMY : sr.dst[c] + 4 * j * SW + v] = sr.vals[c][j][v];
+}
+"""
+PATCHES["lk_rg"] = [
+    ("lookup_stage.h", "// Exact direct gather of one sample of query p", LK_RG_FN + "\n// Exact direct gather of one sample of query p"),
+    ("lookup.hip", """    __syncthreads();
+    stage_windows<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid);
+""", """    __syncthreads();
+    if constexpr (PAIR) {
+        StageRegsRG<R, QB, NTQ> sr;
+        stage_issue_rg<R, QB, NTQ>(st, P, lv, b, q0, tid, sr);
+        stage_commit_rg<R, QB, NTQ>(st, sr, tid);
+        __syncthreads();
+    } else {
+        stage_windows<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid);
+    }
+""")]
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
