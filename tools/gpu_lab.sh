@@ -26,10 +26,13 @@ if [ -n "$ABT" ]; then
   AB_NOCHECK=1 AB_ALT_LIB=${L#,} timeout -k 10 400 python -u tools/ab_build.py > $OUT/abt.log 2>&1
   rc=$?; echo "abt rc=$rc"; grep median $OUT/abt.log; [ $rc -ne 0 ] && exit $rc
 fi
-for n in $LK; do
-  AB_ALT_LIB=$n=tools/${n}_lab/e-raft_amd/libecorr.so timeout -k 10 300 python -u tools/ab_lookup.py > $OUT/lk_$n.log 2>&1
-  rc=$?; echo "lk $n rc=$rc"; grep -E "DIFFERENT|differs|median" $OUT/lk_$n.log | tail -8; [ $rc -ne 0 ] && exit $rc
-done
+if [ -n "$LK" ]; then   # all lookup labs in one process per coordinate field (smooth, i.i.d. sigma 3)
+  L=""; for n in $LK; do L="$L,$n=tools/${n}_lab/e-raft_amd/libecorr.so"; done
+  for f in smooth iid3; do
+    AB_COORDS=$f AB_ALT_LIB=${L#,} timeout -k 10 300 python -u tools/ab_lookup.py > $OUT/lk_$f.log 2>&1
+    rc=$?; echo "lk $f rc=$rc"; grep -E "DIFFERENT|differs|median" $OUT/lk_$f.log | tail -8; [ $rc -ne 0 ] && exit $rc
+  done
+fi
 for n in $STAMPS; do   # build stamps labs (tools/stamps16.py)
   timeout -k 10 120 python -u tools/stamps16.py tools/${n}_lab/e-raft_amd/libecorr.so > $OUT/stamps_$n.log 2>&1
   rc=$?; echo "stamps $n rc=$rc"; cat $OUT/stamps_$n.log | tail -7; [ $rc -ne 0 ] && exit $rc
