@@ -20,8 +20,9 @@ from eraft_amd import _lib  # noqa: E402
 
 L = ctypes.CDLL(os.path.join(ROOT, sys.argv[1]))
 for name, (res, args) in _lib.SYMBOLS.items():
-    getattr(L, name).restype = res
-    getattr(L, name).argtypes = args
+    if hasattr(L, name):   # (a lab build of an older ABI lacks later symbols)
+        getattr(L, name).restype = res
+        getattr(L, name).argtypes = args
 _lib._lib = L
 field = sys.argv[2] if len(sys.argv) > 2 else "smooth"
 B, H, W = 16, 60, 80

@@ -18,8 +18,9 @@ B, H, W = (int(x) for x in sys.argv[3:6]) if len(sys.argv) > 5 else (16, 60, 80)
 if lib != "tree":
     L = ctypes.CDLL(os.path.join(ROOT, lib))
     for name, (res, args) in _lib.SYMBOLS.items():
-        getattr(L, name).restype = res
-        getattr(L, name).argtypes = args
+        if hasattr(L, name):   # (a lab build of an older ABI lacks later symbols)
+            getattr(L, name).restype = res
+            getattr(L, name).argtypes = args
     _lib._lib = L
 g = torch.Generator(device="cuda").manual_seed(0)
 with torch.no_grad():
