@@ -728,6 +728,87 @@ PATCHES["lk_rg"] = [
     }
 """)]
 
+# ---- round 4: persistent lookup -- a grid of 5 workgroups per CU (the LDS limit) walks the units
+# (64-query group, level, batch item) round robin, and each unit's coordinates are loaded one unit
+# ahead (phase 0 was 1.9 us of a ~8 us workgroup life, most of it the coordinate load's latency)
+PATCHES["lk_pers"] = [
+    ("lookup.hip", """template <int R, int QB, bool PAIR>
+__global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
+    constexpr int NTQ = 3 * QB, K = 2 * R + 1, AP = K / 3;
+    static_assert(K % 3 == 0 && QB == kWave, "one wave per part, whole columns per part");
+    using WB = WindowBuf<R, QB, PAIR>;
+    constexpr int S = WB::S, SW = WB::SW, SP = WB::SP, KK = WB::KK;
+    __shared__ WB st;
+    const int tid = threadIdx.x, g = tid % QB;
+    const int part = __builtin_amdgcn_readfirstlane(tid / QB);   // wave-uniform
+    const int lv = blockIdx.y, b = blockIdx.z;
+    const int q0 = blockIdx.x * QB;""", """template <int R, int QB, bool PAIR>
+__device__ __forceinline__ void lookup_cols_unit(const LookupParams& P, WindowBuf<R, QB, PAIR>& st, int lv, int b,
+                                                 int q0, float cxraw, float cyraw) {
+    constexpr int NTQ = 3 * QB, K = 2 * R + 1, AP = K / 3;
+    static_assert(K % 3 == 0 && QB == kWave, "one wave per part, whole columns per part");
+    using WB = WindowBuf<R, QB, PAIR>;
+    constexpr int S = WB::S, SW = WB::SW, SP = WB::SP, KK = WB::KK;
+    const int tid = threadIdx.x, g = tid % QB;
+    const int part = __builtin_amdgcn_readfirstlane(tid / QB);   // wave-uniform"""),
+    ("lookup.hip", """        const float cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
+        const float cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);
+        const float wm1 = (float)(P.lw[lv] - 1), hm1 = (float)(P.lh[lv] - 1);
+#pragma unroll
+        for (int bb = 0; bb < K; ++bb) coord_chain<R>(cy, bb, hm1, fy[bb], wy[bb]);""", """        (void)Q;
+        const float cx = __fmul_rn(cxraw, inv);
+        const float cy = __fmul_rn(cyraw, inv);
+        const float wm1 = (float)(P.lw[lv] - 1), hm1 = (float)(P.lh[lv] - 1);
+#pragma unroll
+        for (int bb = 0; bb < K; ++bb) coord_chain<R>(cy, bb, hm1, fy[bb], wy[bb]);"""),
+    ("lookup.hip", """// Any radius: one thread per output element, direct gather""", """template <int R, int QB, bool PAIR>
+__global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P, int nqg, int units) {
+    __shared__ WindowBuf<R, QB, PAIR> st;
+    const int g = threadIdx.x % QB;
+    auto coords_of = [&](int uu, float& cx, float& cy) {
+        cx = cy = 0.0f;
+        if (uu < units) {
+            const int bb = uu / nqg / P.levels, p = (uu % nqg) * QB + g;
+            if (p < P.q_count) {
+                cx = P.coords[((int64_t)bb * 2 + 0) * P.q_count + p];
+                cy = P.coords[((int64_t)bb * 2 + 1) * P.q_count + p];
+            }
+        }
+    };
+    int u = blockIdx.x;
+    float cx, cy;
+    coords_of(u, cx, cy);
+    while (u < units) {
+        const int un = u + (int)gridDim.x;
+        float ncx, ncy;
+        coords_of(un, ncx, ncy);   // in flight during this unit
+        const int r = u / nqg;
+        lookup_cols_unit<R, QB, PAIR>(P, st, r % P.levels, r / P.levels, (u % nqg) * QB, cx, cy);
+        u = un;
+        cx = ncx;
+        cy = ncy;
+    }
+}
+
+// Any radius: one thread per output element, direct gather"""),
+    ("lookup.hip", """    if (cols) {
+        bool pair = true;""", """    if (cols) {
+        const int nqg = (P.q_count + 63) / 64, units = nqg * P.levels * B;
+        const dim3 grid(units < 1280 ? units : 1280);
+        bool pair = true;"""),
+    ("lookup.hip", """            if (pair) hipLaunchKernelGGL((lookup_cols_reg<4, 64, true>), grid, dim3(192), 0, stream, P);
+            else hipLaunchKernelGGL((lookup_cols_reg<4, 64, false>), grid, dim3(192), 0, stream, P);
+        } else {
+            if (pair) hipLaunchKernelGGL((lookup_cols_reg<1, 64, true>), grid, dim3(192), 0, stream, P);
+            else hipLaunchKernelGGL((lookup_cols_reg<1, 64, false>), grid, dim3(192), 0, stream, P);""",
+     """            if (pair) hipLaunchKernelGGL((lookup_cols_reg<4, 64, true>), grid, dim3(192), 0, stream, P, nqg, units);
+            else hipLaunchKernelGGL((lookup_cols_reg<4, 64, false>), grid, dim3(192), 0, stream, P, nqg, units);
+        } else {
+            if (pair) hipLaunchKernelGGL((lookup_cols_reg<1, 64, true>), grid, dim3(192), 0, stream, P, nqg, units);
+            else hipLaunchKernelGGL((lookup_cols_reg<1, 64, false>), grid, dim3(192), 0, stream, P, nqg, units);"""),
+]
+
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
