@@ -809,6 +809,82 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P, int nq
 ]
 
 
+# ---- lk_persd: lk_pers with a dynamic work queue (one device counter slot per launch, reset by
+# the workgroup that takes the last id) instead of round robin
+PATCHES["lk_persd"] = [(f, o, n) for f, o, n in PATCHES["lk_pers"] if "lookup_cols_unit<R, QB, PAIR>(P, st" not in n
+                       and "const dim3 grid(units < 1280" not in n and "stream, P, nqg, units);" not in n] + [
+    ("lookup.hip", """// Any radius: one thread per output element, direct gather""", """__device__ unsigned int g_lkq[4096];
+
+template <int R, int QB, bool PAIR>
+__global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P, int nqg, int units, unsigned int* ctr) {
+    __shared__ WindowBuf<R, QB, PAIR> st;
+    __shared__ int next_u;
+    const int g = threadIdx.x % QB;
+    auto coords_of = [&](int uu, float& cx, float& cy) {
+        cx = cy = 0.0f;
+        if (uu < units) {
+            const int bb = uu / nqg / P.levels, p = (uu % nqg) * QB + g;
+            if (p < P.q_count) {
+                cx = P.coords[((int64_t)bb * 2 + 0) * P.q_count + p];
+                cy = P.coords[((int64_t)bb * 2 + 1) * P.q_count + p];
+            }
+        }
+    };
+    int u = blockIdx.x;
+    if (u >= units) return;
+    float cx, cy;
+    coords_of(u, cx, cy);
+    while (true) {
+        unsigned int old = 0;
+        if (threadIdx.x == 0) {   // the next unit, taken now, published after this unit's staging
+            old = atomicAdd(ctr, 1u);
+            if (old == (unsigned)units - 1u) atomicExch(ctr, 0u);   // the last id of the launch: reset the slot
+        }
+        const int r = u / nqg;
+        lookup_cols_unit<R, QB, PAIR>(P, st, r % P.levels, r / P.levels, (u % nqg) * QB, cx, cy, &next_u,
+                                      (int)gridDim.x + (int)old);
+        const int un = next_u;   // written before the unit's staging barrier, read after it
+        if (un >= units) break;
+        u = un;
+        coords_of(u, cx, cy);
+    }
+}
+
+// Any radius: one thread per output element, direct gather"""),
+    ("lookup.hip", """                                                 int q0, float cxraw, float cyraw) {""",
+     """                                                 int q0, float cxraw, float cyraw, int* next_u, int nxt) {"""),
+    ("lookup.hip", """    __syncthreads();
+    stage_windows<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid);
+""", """    __syncthreads();
+    {
+        StageRegs<R, QB, NTQ, PAIR> sr;
+        stage_issue<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid, sr);
+        stage_commit<R, QB, NTQ, PAIR>(st, sr);
+        if (tid == 0) *next_u = nxt;
+        __syncthreads();
+    }
+"""),
+    ("lookup.hip", """    if (cols) {
+        bool pair = true;""", """    if (cols) {
+        static unsigned slot_seq = 0;
+        unsigned int* q = nullptr;
+        if (hipGetSymbolAddress((void**)&q, HIP_SYMBOL(g_lkq)) != hipSuccess) return ECORR_EINVAL;
+        q += (slot_seq++) % 4096;
+        const int nqg = (P.q_count + 63) / 64, units = nqg * P.levels * B;
+        const dim3 grid(units < 1280 ? units : 1280);
+        bool pair = true;"""),
+    ("lookup.hip", """            if (pair) hipLaunchKernelGGL((lookup_cols_reg<4, 64, true>), grid, dim3(192), 0, stream, P);
+            else hipLaunchKernelGGL((lookup_cols_reg<4, 64, false>), grid, dim3(192), 0, stream, P);
+        } else {
+            if (pair) hipLaunchKernelGGL((lookup_cols_reg<1, 64, true>), grid, dim3(192), 0, stream, P);
+            else hipLaunchKernelGGL((lookup_cols_reg<1, 64, false>), grid, dim3(192), 0, stream, P);""",
+     """            if (pair) hipLaunchKernelGGL((lookup_cols_reg<4, 64, true>), grid, dim3(192), 0, stream, P, nqg, units, q);
+            else hipLaunchKernelGGL((lookup_cols_reg<4, 64, false>), grid, dim3(192), 0, stream, P, nqg, units, q);
+        } else {
+            if (pair) hipLaunchKernelGGL((lookup_cols_reg<1, 64, true>), grid, dim3(192), 0, stream, P, nqg, units, q);
+            else hipLaunchKernelGGL((lookup_cols_reg<1, 64, false>), grid, dim3(192), 0, stream, P, nqg, units, q);"""),
+]
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
