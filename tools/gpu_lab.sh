@@ -33,6 +33,11 @@ if [ -n "$LK" ]; then   # all lookup labs in one process per coordinate field (s
     rc=$?; echo "lk $f rc=$rc"; grep -E "DIFFERENT|differs|median" $OUT/lk_$f.log | tail -8; [ $rc -ne 0 ] && exit $rc
   done
 fi
+if [ -n "$MO" ]; then   # fused lookup + convc1 labs, one process
+  L=""; for n in $MO; do L="$L,$n=tools/${n}_lab/e-raft_amd/libecorr.so"; done
+  AB_ALT_LIB=${L#,} timeout -k 10 300 python -u tools/ab_motion.py > $OUT/mo.log 2>&1
+  rc=$?; echo "mo rc=$rc"; grep -E "DIFFERENT|differs|median" $OUT/mo.log | tail -8; [ $rc -ne 0 ] && exit $rc
+fi
 for n in $STAMPS; do   # build stamps labs (tools/stamps16.py)
   timeout -k 10 120 python -u tools/stamps16.py tools/${n}_lab/e-raft_amd/libecorr.so > $OUT/stamps_$n.log 2>&1
   rc=$?; echo "stamps $n rc=$rc"; cat $OUT/stamps_$n.log | tail -7; [ $rc -ne 0 ] && exit $rc

@@ -885,6 +885,19 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P, int nq
             else hipLaunchKernelGGL((lookup_cols_reg<1, 64, false>), grid, dim3(192), 0, stream, P, nqg, units, q);"""),
 ]
 
+# ---- round 4: fused lookup + convc1, second resident workgroup of each CU in the first dispatch
+# round (linear ids 256..511: CU-breadth-first placement) started late by ~N x 4 us, so one
+# workgroup's lookup phase runs beside the other's GEMM phase instead of in step with it
+for _n in (1, 3, 6):
+    PATCHES[f"mo_stag{_n}"] = [("motion.hip", """    const int tid = threadIdx.x, g = tid % QBM, part = tid / QBM, lane = tid & 63, wave = tid >> 6;
+    const int half = part & 1;""", f"""    {{
+        const unsigned lin = blockIdx.x + gridDim.x * blockIdx.y;
+        if (lin >= 256 && lin < 512)
+            for (int z = 0; z < {_n}; ++z) __builtin_amdgcn_s_sleep(127);
+    }}
+    const int tid = threadIdx.x, g = tid % QBM, part = tid / QBM, lane = tid & 63, wave = tid >> 6;
+    const int half = part & 1;""")]
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
