@@ -69,18 +69,19 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
     const int p = q0 + g;
     const bool valid = p < P.q_count;
 
-    // ---- phase 0 (registers): this thread's chains
+    // ---- phase 0 (registers): the window's end-point chains (the origin needs only those); the
+    // other chains are computed under the staging loads' latency (round 4: 41.7-41.9 vs 42.0-42.3 us
+    // smooth, 45.7-46.0 vs 45.9-46.2 us i.i.d., profiles/r04_lab/)
     float fy[K], wy[K], fx[AP], wx[AP], x0 = 0.0f, xl = 0.0f;
+    float cx = 0.0f, cy = 0.0f;
+    const float wm1 = (float)(P.lw[lv] - 1), hm1 = (float)(P.lh[lv] - 1);
     if (valid) {
         const int64_t Q = P.q_count;
         const float inv = 1.0f / (float)(1 << lv);  // coords / 2**i is an exact scaling
-        const float cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
-        const float cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);
-        const float wm1 = (float)(P.lw[lv] - 1), hm1 = (float)(P.lh[lv] - 1);
-#pragma unroll
-        for (int bb = 0; bb < K; ++bb) coord_chain<R>(cy, bb, hm1, fy[bb], wy[bb]);
-#pragma unroll
-        for (int ai = 0; ai < AP; ++ai) coord_chain<R>(cx, part * AP + ai, wm1, fx[ai], wx[ai]);
+        cx = __fmul_rn(P.coords[((int64_t)b * 2 + 0) * Q + p], inv);
+        cy = __fmul_rn(P.coords[((int64_t)b * 2 + 1) * Q + p], inv);
+        coord_chain<R>(cy, 0, hm1, fy[0], wy[0]);
+        coord_chain<R>(cy, K - 1, hm1, fy[K - 1], wy[K - 1]);
         float dummy;
         coord_chain<R>(cx, 0, wm1, x0, dummy);
         coord_chain<R>(cx, K - 1, wm1, xl, dummy);
@@ -93,7 +94,18 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
         st.org[g][2] = org[2];
     }
     __syncthreads();
-    stage_windows<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid);
+    {
+        StageRegs<R, QB, NTQ, PAIR> sr;
+        stage_issue<R, QB, NTQ, PAIR>(st, P, lv, b, q0, tid, sr);
+        if (valid) {   // the remaining chains under the staging loads' latency
+#pragma unroll
+            for (int bb = 1; bb < K - 1; ++bb) coord_chain<R>(cy, bb, hm1, fy[bb], wy[bb]);
+#pragma unroll
+            for (int ai = 0; ai < AP; ++ai) coord_chain<R>(cx, part * AP + ai, wm1, fx[ai], wx[ai]);
+        }
+        stage_commit<R, QB, NTQ, PAIR>(st, sr);
+        __syncthreads();
+    }
 
     const int md = org[2] & 0xff;
     if (md == 2) return;   // past the range (no barrier follows)
