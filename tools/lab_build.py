@@ -898,6 +898,52 @@ for _n in (1, 3, 6):
     const int tid = threadIdx.x, g = tid % QBM, part = tid / QBM, lane = tid & 63, wave = tid >> 6;
     const int half = part & 1;""")]
 
+# ---- round 4: persistent split16 build -- 512 blocks (two per CU) walk the tiles, one barrier
+# between a block's tiles; would measure what the per-block dispatch gaps cost (bitwise the same).
+# Not run: the tile loop pushes the kernel to 256 VGPRs + 204 B/lane of scratch spills.
+PATCHES["s16_pers"] = [
+    ("build.hip", """template <bool MUL>
+__global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
+    // ALL LDS in this one array (cdna_hip_programming.md trap 4(a), see build_split_kernel)
+    __shared__ __attribute__((aligned(16))) char smem[SLDS + (SQ + 256) * 4];
+    int* exq""", """template <bool MUL>
+__device__ __forceinline__ void split16_tile(const BuildParams& P, char* smem, int tile) {
+    int* exq"""),
+    ("build.hip", """    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    const NTile tc = ntile_of(P, nt);
+    const int q0 = qt * SQ;
+    const int H = P.H, W = P.W;
+    const int64_t Q = (int64_t)H * W;
+
+    // per-pixel exponents: loaded behind the K loop's last static wait (only the epilogue reads them)""",
+     """    decode_tile(P, tile, P.n_qt, b, qt, nt);
+    const NTile tc = ntile_of(P, nt);
+    const int q0 = qt * SQ;
+    const int H = P.H, W = P.W;
+    const int64_t Q = (int64_t)H * W;
+
+    // per-pixel exponents: loaded behind the K loop's last static wait (only the epilogue reads them)"""),
+    ("build.hip", """        split16_epilogue<MUL, false>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+}
+""", """        split16_epilogue<MUL, false>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+}
+
+template <bool MUL>
+__global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P, int ntiles) {
+    __shared__ __attribute__((aligned(16))) char smem[SLDS + (SQ + 256) * 4];
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        split16_tile<MUL>(P, smem, xcd_remap(t, ntiles));
+        __syncthreads();   // every wave's epilogue is done with the panel buffers
+    }
+}
+"""),
+    ("build.hip", """            if (P.scale_is_mul) hipLaunchKernelGGL((build_split16_kernel<true>), grid, dim3(256), 0, stream, P);
+            else hipLaunchKernelGGL((build_split16_kernel<false>), grid, dim3(256), 0, stream, P);""",
+     """            const dim3 pg((unsigned)(ntiles < 512 ? ntiles : 512));
+            if (P.scale_is_mul) hipLaunchKernelGGL((build_split16_kernel<true>), pg, dim3(256), 0, stream, P, (int)ntiles);
+            else hipLaunchKernelGGL((build_split16_kernel<false>), pg, dim3(256), 0, stream, P, (int)ntiles);"""),
+]
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
