@@ -759,7 +759,11 @@ def main():
                                 other_roof={k: other[k] for k in ("bound", "achieved", "peak", "unit", "frac")})
     kernels["lookup"] = {"bound": "hbm", "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(look_gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(look_ms, 4),
-                         "launches_per_step": iters, "work_per_launch": f"{look_bytes:.4g} B" + note}
+                         "launches_per_step": iters, "work_per_launch": f"{look_bytes:.4g} B" + note,
+                         "covers": ("a step's 12 lookups / 12, from its GEMM's end event to the next step's "
+                                    "operand-pass event (the last step: its closing event) -- kernel boundaries "
+                                    "and any host gap before the next step's first launch included" if lean else
+                                    "a step's 12 lookups / 12 between two HIP events")}
 
     def spread_seq(xs):   # min / median / max and the first and last of the sequence
         if not xs:
