@@ -944,6 +944,16 @@ __global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P, in
             else hipLaunchKernelGGL((build_split16_kernel<false>), pg, dim3(256), 0, stream, P, (int)ntiles);"""),
 ]
 
+# ---- round 4: convex upsampling with the softmax's 9 IEEE divisions replaced by one reciprocal
+# and 9 multiplies (up_rcp), and + the fast exp (up_fast: __expf); normwise within the test bar
+PATCHES["up_rcp"] = [("upsample.hip", """#pragma unroll
+        for (int k = 0; k < 9; ++k) m[k] = __fdiv_rn(m[k], s);   // softmax output""",
+                      """        const float rs = __builtin_amdgcn_rcpf(s);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) m[k] = __fmul_rn(m[k], rs);   // softmax output""")]
+PATCHES["up_fast"] = PATCHES["up_rcp"] + [("upsample.hip", "            m[k] = expf(__fsub_rn(m[k], mx));",
+                                           "            m[k] = __expf(__fsub_rn(m[k], mx));")]
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
