@@ -11,9 +11,11 @@
 // comes from L1/L2, and the 8 sub-pixels j of a row leave as two float4 stores (a wave writes
 // 64 x 32 contiguous bytes).  HBM-bound: 2304 B of mask in + 512 B of flow out per pixel.
 //
-// Numerics: softmax as max, exp(x - max), in-order sum, divide; then the in-order sum of the 9
-// products -- the reference's expression order; exp is the device's expf (<= 1 ulp), so results
-// agree with the reference within a few ulp rather than bit for bit.
+// Numerics: softmax as max, exp(x - max), in-order sum, times the sum's reciprocal; then the
+// in-order sum of the 9 products -- the reference's expression order.  exp is the hardware's
+// exp2-based __expf and the division a v_rcp_f32 multiply (round 4: 42.9 vs 51.8 us per call at
+// DSEC B=16, profiles/r04_lab/; normwise error vs an fp64 evaluation unchanged, 1.69e-6), so
+// results agree with the reference within a few ulp rather than bit for bit (test bar 2e-6).
 //
 // DSEC submission codec (utils/visualization.py:75-93, utils/dsec_utils.py:66-83):
 //   encode  uint16[h][w][3] = (u16)(int32)rint(flow * 128 + 2^15), channel 2 = 0 -- numpy's
@@ -66,11 +68,12 @@ __global__ __launch_bounds__(NTU) void upsample_kernel(const float* __restrict__
         float s = 0.0f;
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
-            m[k] = expf(__fsub_rn(m[k], mx));
+            m[k] = __expf(__fsub_rn(m[k], mx));
             s = __fadd_rn(s, m[k]);
         }
+        const float rs = __builtin_amdgcn_rcpf(s);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) m[k] = __fdiv_rn(m[k], s);   // softmax output
+        for (int k = 0; k < 9; ++k) m[k] = __fmul_rn(m[k], rs);   // softmax output
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             float acc = 0.0f;

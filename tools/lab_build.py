@@ -954,6 +954,9 @@ PATCHES["up_rcp"] = [("upsample.hip", """#pragma unroll
 PATCHES["up_fast"] = PATCHES["up_rcp"] + [("upsample.hip", "            m[k] = expf(__fsub_rn(m[k], mx));",
                                            "            m[k] = __expf(__fsub_rn(m[k], mx));")]
 
+# ---- round 4: the fused lookup + convc1 as the two-workgroup kernel (the tree: warp-specialized)
+PATCHES["mo_2wg"] = [("motion.hip", "constexpr bool kConvWS = true;", "constexpr bool kConvWS = false;")]
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
