@@ -43,6 +43,10 @@ if [ -n "$UP" ]; then   # convex upsampling labs, one process
   AB_ALT_LIB=${L#,} timeout -k 10 300 python -u tools/ab_upsample.py > $OUT/up.log 2>&1
   rc=$?; echo "up rc=$rc"; grep -E "normwise|median" $OUT/up.log | tail -8; [ $rc -ne 0 ] && exit $rc
 fi
+for n in $MOSTAMPS; do
+  timeout -k 10 120 python -u tools/mostamps.py tools/${n}_lab/e-raft_amd/libecorr.so > $OUT/mostamps_$n.log 2>&1
+  rc=$?; echo "mostamps $n rc=$rc"; tail -4 $OUT/mostamps_$n.log; [ $rc -ne 0 ] && exit $rc
+done
 for n in $STAMPS; do   # build stamps labs (tools/stamps16.py)
   timeout -k 10 120 python -u tools/stamps16.py tools/${n}_lab/e-raft_amd/libecorr.so > $OUT/stamps_$n.log 2>&1
   rc=$?; echo "stamps $n rc=$rc"; cat $OUT/stamps_$n.log | tail -7; [ $rc -ne 0 ] && exit $rc

@@ -957,6 +957,60 @@ PATCHES["up_fast"] = PATCHES["up_rcp"] + [("upsample.hip", "            m[k] = e
 # ---- round 4: the fused lookup + convc1 as the two-workgroup kernel (the tree: warp-specialized)
 PATCHES["mo_2wg"] = [("motion.hip", "constexpr bool kConvWS = true;", "constexpr bool kConvWS = false;")]
 
+# ---- round 4: stamps of the warp-specialized fused kernel: per workgroup, the cycles its producer
+# wave 0 spends in produce(), its consumer wave 4 in consume(), both in the barrier, and the steps
+MO_DECL = """
+__device__ unsigned long long g_mo[4096][8];
+"""
+MO_EXPORT = """
+extern "C" __attribute__((visibility("default"))) int ecorr_lab_mostamps(void* dst, int n) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ecorr::g_mo), (size_t)n * 64, 0, hipMemcpyDeviceToHost);
+}
+"""
+PATCHES["mo_wsst"] = [
+    ("motion.hip", "constexpr int KC = 16;     // channels per weight chunk", "constexpr int KC = 16;     // channels per weight chunk" + MO_DECL),
+    ("motion.hip", """    const int t0 = (int)blockIdx.x;
+    if (wave < 4) load_coords(t0);
+    for (int k = 0; t0 + (k - 1) * G < ntiles; ++k) {
+        const int t = t0 + k * G;
+        if (wave < 4) {
+            if (t < ntiles) produce(t, k & 1);
+        } else if (k > 0) {
+            consume(t - G, (k - 1) & 1);
+        }
+        __syncthreads();   // the buffers swap roles
+    }
+}""", """    const int t0 = (int)blockIdx.x;
+    if (wave < 4) load_coords(t0);
+    unsigned long long busy = 0, waitc = 0, steps = 0;
+    const unsigned long long tstart = __builtin_amdgcn_s_memtime();
+    for (int k = 0; t0 + (k - 1) * G < ntiles; ++k) {
+        const int t = t0 + k * G;
+        const unsigned long long a0 = __builtin_amdgcn_s_memtime();
+        if (wave < 4) {
+            if (t < ntiles) produce(t, k & 1);
+        } else if (k > 0) {
+            consume(t - G, (k - 1) & 1);
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long a1 = __builtin_amdgcn_s_memtime();
+        __syncthreads();   // the buffers swap roles
+        const unsigned long long a2 = __builtin_amdgcn_s_memtime();
+        busy += a1 - a0;
+        waitc += a2 - a1;
+        ++steps;
+    }
+    if (lane == 0 && (wave == 0 || wave == 4) && blockIdx.x < 4096) {
+        const int o = wave == 0 ? 0 : 3;
+        g_mo[blockIdx.x][o + 0] = busy;
+        g_mo[blockIdx.x][o + 1] = waitc;
+        g_mo[blockIdx.x][o + 2] = steps;
+        if (wave == 0) g_mo[blockIdx.x][6] = __builtin_amdgcn_s_memtime() - tstart;
+    }
+}"""),
+    ("motion.hip", "}  // namespace ecorr\\n", "}  // namespace ecorr\\n" + MO_EXPORT),
+]
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
