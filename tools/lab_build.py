@@ -1008,7 +1008,7 @@ PATCHES["mo_wsst"] = [
         if (wave == 0) g_mo[blockIdx.x][6] = __builtin_amdgcn_s_memtime() - tstart;
     }
 }"""),
-    ("motion.hip", "}  // namespace ecorr\\n", "}  // namespace ecorr\\n" + MO_EXPORT),
+    ("motion.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + MO_EXPORT),
 ]
 
 
