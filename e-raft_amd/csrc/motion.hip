@@ -235,7 +235,7 @@ static_assert(WS_SP % 2 == 1 && 8 * WS_NJ >= WS_S * 6, "window geometry");
 struct WsLds {
     float T[2][WS_CPAD][WS_TS];             // the two corr tiles (rows >= 324 stay zero)
     float win[4][2][WS_WIN];                // per producer wave, two levels in flight
-    float ch[4][2][WS_QP][4][9];            // per producer wave and level parity: fx, wx, fy, wy
+    float ch[4][WS_L][WS_QP][4][9];         // per producer wave and level: fx, wx, fy, wy
 };
 
 __global__ __launch_bounds__(WS_NT, 1) void lookup_conv_ws_kernel(LookupParams P, const float* __restrict__ wt,
@@ -277,8 +277,8 @@ __global__ __launch_bounds__(WS_NT, 1) void lookup_conv_ws_kernel(LookupParams P
         const int64_t g0 = R0 >> 6;
         const int nq = min(QBM, P.q_count - q0t);
         const int64_t Rq = R0 + gq;
-        float vals[2][WS_NJ][2];
-        int org[2][3];
+        float vals[WS_L][WS_NJ][2];
+        int org[WS_L][3];
         // level lv into register set s: chains (this lane's part) into LDS, origin, staging loads
         auto issue = [&](int lv, int s) __attribute__((always_inline)) {
             const float inv = 1.0f / (float)(1 << lv);   // coords / 2**i: exact
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(WS_NT, 1) void lookup_conv_ws_kernel(LookupParams P
             const int h = P.lh[lv], w = P.lw[lv], ntx = P.lntx[lv];
             const float wm1 = (float)(w - 1), hm1 = (float)(h - 1);
             float fx0 = 0.0f, fx8 = 0.0f, fy0 = 0.0f, fy8 = 0.0f;
-            float* ch = &sh.ch[pw][s][qi][0][0];
+            float* ch = &sh.ch[pw][lv][qi][0][0];
             if (valid) {
                 float f, wg, wx8, wy8, dummy;
                 coord_chain<4>(cx, part, wm1, f, wg);
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(WS_NT, 1) void lookup_conv_ws_kernel(LookupParams P
         };
         // level lv from set s: commit into window s (this wave's), then sample into corr rows
         auto finish = [&](int lv, int s) __attribute__((always_inline)) {
-            float* win = sh.win[pw][s];
+            float* win = sh.win[pw][lv & 1];
             const int odd = org[s][0] & 1;
 #pragma unroll
             for (int j = 0; j < WS_NJ; ++j) {
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(WS_NT, 1) void lookup_conv_ws_kernel(LookupParams P
                 for (int v = 0; v < 2; ++v) win[skip == v ? WS_DUMMY : d + v] = vals[s][j][v];
             }
             // (a wave's LDS accesses are processed in order: the reads below see the writes above)
-            const float* ch = &sh.ch[pw][s][qi][0][0];
+            const float* ch = &sh.ch[pw][lv][qi][0][0];
             const int md = org[s][2] & 0xff;
             const float* wq = win + 1 + qi * WS_SP;
             float* trow = &sh.T[buf][lv * WS_KK][gq];
@@ -383,16 +383,17 @@ __global__ __launch_bounds__(WS_NT, 1) void lookup_conv_ws_kernel(LookupParams P
                 }
             }
         };
-        // levels software-pipelined two register sets deep; the loop body handles two levels so
-        // the sets stay compile-time (rolled: four copies of the level code overflow the I-cache)
+        // all four levels' staging loads in flight at once (one memory latency per tile; a lone
+        // producer wave per SIMD exposed two to three in a row), then commit and sample level by
+        // level through two windows
         issue(0, 0);
-#pragma unroll 1
-        for (int lv = 1; lv < WS_L; lv += 2) {
-            issue(lv, 1);
-            finish(lv - 1, 0);
-            if (lv + 1 < WS_L) issue(lv + 1, 0);
-            finish(lv, 1);
-        }
+        issue(1, 1);
+        issue(2, 2);
+        issue(3, 3);
+        finish(0, 0);
+        finish(1, 1);
+        finish(2, 2);
+        finish(3, 3);
     };
 
     // ======================= consumers: the convc1 GEMM of one tile =======================
@@ -404,8 +405,7 @@ __global__ __launch_bounds__(WS_NT, 1) void lookup_conv_ws_kernel(LookupParams P
         const int b = t / nqt, q0t = (t - b * nqt) * QBM;
         for (int oc = 0; oc < O; oc += OB) {
             const int ob = oc + cw * OW;
-            floatx4 wc[4], wn[4];
-            auto load_w = [&](floatx4 (&w)[4], int kc) {
+            auto load_w = [&](floatx4 (&w)[4], int kc) __attribute__((always_inline)) {
                 const bool in = kc < pnkc;
                 const int base = __builtin_amdgcn_readfirstlane(in ? (((ob / OW) * pnkc + kc) * 4) * 1024 : 0);
 #pragma unroll
@@ -416,20 +416,40 @@ __global__ __launch_bounds__(WS_NT, 1) void lookup_conv_ws_kernel(LookupParams P
             floatx16 acc0, acc1;
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc0[r] = 0.0f; acc1[r] = 0.0f; }
-            load_w(wc, 0);
-#pragma unroll 1
-            for (int kc = 0; kc < nkc; ++kc) {
-                if (kc + 1 < nkc) load_w(wn, kc + 1);
-                float bq[8];
+            // one consumer wave per SIMD: the weight two chunks ahead (three register sets) and the
+            // corr-tile operand one chunk ahead hide the L2 and LDS latencies a lone wave exposes
+            floatx4 w3[3][4];
+            float bq[2][8];
+            auto load_b = [&](float (&bb)[8], int kc) __attribute__((always_inline)) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) bq[j] = sh.T[buf][kc * KC + 8 * kr + j][col];
+                for (int j = 0; j < 8; ++j) bb[j] = sh.T[buf][kc * KC + 8 * kr + j][col];
+            };
+            auto chunk = [&](const floatx4 (&w)[4], const float (&bb)[8]) __attribute__((always_inline)) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[j >> 2][j & 3], bq[j], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[2 + (j >> 2)][j & 3], bq[j], acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(w[j >> 2][j & 3], bb[j], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(w[2 + (j >> 2)][j & 3], bb[j], acc1, 0, 0, 0);
                 }
+            };
+            static_assert(WS_CPAD / KC % 3 == 0, "chunks in threes");
+            load_w(w3[0], 0);
+            load_w(w3[1], 1);
+            load_b(bq[0], 0);
+#pragma unroll 1
+            for (int kc = 0; kc < nkc; kc += 3) {
+                load_w(w3[2], kc + 2);
+                load_b(bq[1], kc + 1);
+                chunk(w3[0], bq[0]);
+                if (kc + 3 < nkc) load_w(w3[0], kc + 3);
+                load_b(bq[0], kc + 2);
+                chunk(w3[1], bq[1]);
+                if (kc + 4 < nkc) load_w(w3[1], kc + 4);
+                if (kc + 3 < nkc) load_b(bq[1], kc + 3);
+                chunk(w3[2], bq[0]);
+                if (kc + 3 < nkc) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) wc[i] = wn[i];
+                    for (int j = 0; j < 8; ++j) bq[0][j] = bq[1][j];
+                }
             }
             const int q = q0t + col;
             if (q < P.q_count && ob < O) {
