@@ -247,35 +247,60 @@ def cpu_baseline(f1, f2, coords, iters):
 
 
 def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
-    """fused lookup + convc1 + ReLU (ecorr_lookup_conv1x1_relu) against the
-    unfused path it replaces (our lookup, then torch's conv2d + relu on MIOpen), 12 iterations,
-    HIP events on the launch stream; outside the headline timed region."""
+    """lookup + convc1 + ReLU (CorrBlock.lookup_conv1x1_relu) in both modes --
+    "split" (the default: ecorr_lookup, then the split-f16 ecorr_conv1x1_relu_split) and "fused"
+    (ecorr_lookup_conv1x1_relu_packed, one fp32-MFMA kernel) -- against the unfused path they replace
+    (our lookup, then torch's conv2d + relu on MIOpen), 12 iterations, HIP events on the launch
+    stream; outside the headline timed region.  `conv_split` times the split conv kernel alone on
+    one materialized lookup (HBM-bound: corr in + out)."""
     import torch.nn.functional as F
+    from eraft_amd import _lib
     g = torch.Generator(device=device).manual_seed(99)
     wgt = torch.randn((256, 324, 1, 1), generator=g, device=device) * 0.05
     bias = torch.randn((256,), generator=g, device=device) * 0.1
     stream = torch.cuda.current_stream(device)
 
-    def run(fn):
+    def run(fn, n=len(coords)):
         ts = []
         for _ in range(reps + 1):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            for c in coords:
-                fn(c)
+            for i in range(n):
+                fn(coords[i % len(coords)])
             e1.record(stream)
             torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1) / len(coords))
+            ts.append(e0.elapsed_time(e1) / n)
         return sorted(ts[1:])[len(ts[1:]) // 2]
 
+    Q = H * W
     with torch.no_grad():
-        fused = run(lambda c: blk.lookup_conv1x1_relu(c, wgt, bias))
+        fused = run(lambda c: blk.lookup_conv1x1_relu(c, wgt, bias, mode="fused"))
+        split = run(lambda c: blk.lookup_conv1x1_relu(c, wgt, bias, mode="split"))
         unfused = run(lambda c: torch.relu(F.conv2d(blk(c), wgt, bias)))
-    flops = 2.0 * B * H * W * 256 * 324
-    return {"fused_ms_per_iter": round(fused, 4), "unfused_ms_per_iter": round(unfused, 4),
-            "speedup": round(unfused / fused, 3), "bound": "mfma",
-            "achieved": round(flops / (fused * 1e-3) / 1e12, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(flops / (fused * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
+        lookup = run(lambda c: blk(c))
+        corr = blk(coords[0])
+        out = torch.empty((B, 256, H, W), device=device)
+        pk = _lib.packed_conv1x1_weight(wgt, 256, 324, "split")
+        conv = run(lambda c: _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
+            corr.data_ptr(), B, 324, Q, pk.data_ptr(), bias.data_ptr(), 256, out.data_ptr(),
+            _lib.stream_of(corr)), "split conv"))
+    flops = 2.0 * B * Q * 256 * 324
+    conv_bytes = 4.0 * B * Q * (324 + 256)
+    default = os.environ.get("ECORR_CONVC1", "split")
+    best = split if default == "split" else fused
+    return {"mode": default, "ms_per_iter": round(best, 4),
+            "split_ms_per_iter": round(split, 4), "fused_ms_per_iter": round(fused, 4),
+            "unfused_ms_per_iter": round(unfused, 4), "lookup_ms_per_iter": round(lookup, 4),
+            "speedup_vs_unfused": round(unfused / best, 3),
+            "fp32_equiv": {"achieved": round(flops / (best * 1e-3) / 1e12, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
+                           "unit": "TFLOP/s", "frac": round(flops / (best * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
+                           "note": "the conv's 2*O*C flop per query over the whole lookup + convc1 time, "
+                                   "against the fp32 MFMA peak (the split mode runs them as 3 f16 MFMAs each)"},
+            "conv_split": {"ms": round(conv, 4), "bound": "hbm",
+                           "achieved": round(conv_bytes / (conv * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
+                           "unit": "GB/s", "frac": round(conv_bytes / (conv * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                           "bytes": f"{conv_bytes:.4g} B: corr in (324 x 4 B) + out (256 x 4 B) per query "
+                                    "(the kernel reads corr twice: max pre-pass + K loop)"},
             "work_per_launch": f"{flops:.4g} flop (1x1 conv 324->256 over B*H*W queries)"}
 
 

@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -53,6 +53,11 @@ SYMBOLS = {
     "ecorr_conv1x1_packed_size": (_i, [_i, _i, ctypes.POINTER(_i64)]),
     "ecorr_conv1x1_pack": (_i, [_p, _i, _i, _p, _p]),
     "ecorr_lookup_conv1x1_relu_packed": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _p, _p]),
+    # (O, C, bytes*) / (weight[O][C], O, C, packed, stream) /
+    # (in[B][C][Q], B, C, Q, packed, bias, O, out, stream): split-f16 convc1 + ReLU (ABI 15)
+    "ecorr_conv1x1_split_size": (_i, [_i, _i, ctypes.POINTER(_i64)]),
+    "ecorr_conv1x1_split_pack": (_i, [_p, _i, _i, _p, _p]),
+    "ecorr_conv1x1_relu_split": (_i, [_p, _i, _i, _i, _p, _p, _i, _p, _p]),
     "ecorr_bilinear_sampler": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _p]),
     "ecorr_coords_grid": (_i, [_i, _i, _i, _p, _p]),
     # (chunks, chunk, world, B, C, H, W, out, stream)
@@ -212,30 +217,38 @@ def build_pyramid(fmap1, fmap2, B, D, H, W, q_count, levels, off, what, mode=Non
     return pyr
 
 
-# Packed convc1 weights (ecorr_conv1x1_pack) per weight tensor: id -> (weakref, version, O, C, packed).
-# The fused lookup + convc1 kernel reads the weight in its MFMA fragment order; ERAFT.forward calls
-# it `iters` times per forward with the same convc1.weight, so the weight is re-laid once and again
-# only after an in-place update (the tensor's version counter) -- or on every call for tensors
-# without a version counter (inference-mode tensors).
+# Packed convc1 weights per weight tensor: (id, kind) -> (weakref, version, O, C, packed).  kind
+# "fused": ecorr_conv1x1_pack (the fused lookup + convc1 kernel's fp32 MFMA fragment order); "split":
+# ecorr_conv1x1_split_pack (hi/lo f16 fragments + row exponents for ecorr_conv1x1_relu_split).
+# ERAFT.forward calls convc1 `iters` times per forward with the same weight, so the weight is
+# re-laid once and again only after an in-place update (the tensor's version counter) -- or on
+# every call for tensors without a version counter (inference-mode tensors).
 _packed_weights = {}
 
 
-def packed_conv1x1_weight(weight, O, C):
+def packed_conv1x1_weight(weight, O, C, kind="fused"):
     import weakref
     try:
         version = weight._version
     except RuntimeError:   # inference tensor: no version counter, no caching
         version = None
-    key = id(weight)
+    key = (id(weight), kind)
     ent = _packed_weights.get(key)
     if (version is not None and ent is not None and ent[0]() is weight and ent[1] == version
             and ent[2:4] == (O, C) and ent[4].device == weight.device):
         return ent[4]
     wt = weight.reshape(O, C).contiguous()
     n = ctypes.c_int64()
-    check(lib().ecorr_conv1x1_packed_size(O, C, ctypes.byref(n)), "convc1 weight pack")
-    packed = torch.empty(n.value, dtype=torch.float32, device=weight.device)
-    check(lib().ecorr_conv1x1_pack(wt.data_ptr(), O, C, packed.data_ptr(), stream_of(weight)), "convc1 weight pack")
+    if kind == "split":
+        check(lib().ecorr_conv1x1_split_size(O, C, ctypes.byref(n)), "convc1 split weight pack")
+        packed = torch.empty(n.value, dtype=torch.uint8, device=weight.device)
+        check(lib().ecorr_conv1x1_split_pack(wt.data_ptr(), O, C, packed.data_ptr(), stream_of(weight)),
+              "convc1 split weight pack")
+    else:
+        check(lib().ecorr_conv1x1_packed_size(O, C, ctypes.byref(n)), "convc1 weight pack")
+        packed = torch.empty(n.value, dtype=torch.float32, device=weight.device)
+        check(lib().ecorr_conv1x1_pack(wt.data_ptr(), O, C, packed.data_ptr(), stream_of(weight)),
+              "convc1 weight pack")
     if version is not None:
         for k in [k for k, e in _packed_weights.items() if e[0]() is None]:
             del _packed_weights[k]

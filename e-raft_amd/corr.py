@@ -27,6 +27,8 @@ corr_pyramid is a materialized COPY in the reference layout: 4 levels of B*H*W q
 (1.96 GB at DSEC B=16, the whole pyramid again), made on first access and cached on the block.
 Nothing on the E-RAFT path reads it; access it only for inspection or tests.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -106,11 +108,18 @@ class CorrBlock:
                 self.radius, out.data_ptr(), _lib.stream_of(coords)), "CorrBlock lookup")
         return out
 
-    def lookup_conv1x1_relu(self, coords, weight, bias=None):
-        """F.relu(conv1x1(self(coords), weight, bias)) without materializing the lookup: the
-        lookup fused with BasicMotionEncoder.convc1 + ReLU (update.py:67,74).
+    def lookup_conv1x1_relu(self, coords, weight, bias=None, mode=None):
+        """F.relu(conv1x1(self(coords), weight, bias)): the lookup followed by
+        BasicMotionEncoder.convc1 + ReLU (update.py:67,74).
         weight: [O, C, 1, 1] (or [O, C]) fp32 with C = num_levels * (2r+1)^2; bias: [O] or None.
-        Returns [B, O, H, W].  Needs radius 4, num_levels <= 4 and O a multiple of 64."""
+        Returns [B, O, H, W].  mode (default: env ECORR_CONVC1, else "split"):
+          "split"  ecorr_lookup into a temporary [B, C, H, W], then ecorr_conv1x1_relu_split (f16
+                   matrix cores, split operands: normwise within 1e-5 of the fp32 conv);
+          "fused"  ecorr_lookup_conv1x1_relu_packed: one kernel, the lookup tile never leaves the
+                   CU, an exact c-ordered fp32 MFMA sum (radius 4, num_levels <= 4, O a multiple of 64)."""
+        mode = mode or os.environ.get("ECORR_CONVC1", "split")
+        if mode not in ("split", "fused"):
+            raise ValueError(f"mode {mode!r}: expected 'split' or 'fused'")
         B, _, H, W = self._shape
         _require_device_f32("coords", coords)
         _require_device_f32("weight", weight)
@@ -129,16 +138,24 @@ class CorrBlock:
             if bias.numel() != O:
                 raise RuntimeError(f"bias has {bias.numel()} elements, expected {O}")
             bias = bias.contiguous()
-        if O <= 0 or O % 64 != 0:
+        if mode == "fused" and (O <= 0 or O % 64 != 0):
             raise RuntimeError(f"{O} output channels: the fused kernel needs a positive multiple of 64")
         coords = coords.contiguous()
+        bptr = None if bias is None else bias.data_ptr()
         with _lib.on_device(self._device):
-            wt = _lib.packed_conv1x1_weight(weight, O, C)   # MFMA fragment order, re-laid once per weight
             out = torch.empty((B, O, H, W), dtype=torch.float32, device=self._device)
-            _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu_packed(
-                self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, self.num_levels,
-                self.radius, wt.data_ptr(), None if bias is None else bias.data_ptr(), O,
-                out.data_ptr(), _lib.stream_of(coords)), "CorrBlock lookup+conv1x1+relu")
+            st = _lib.stream_of(coords)
+            if mode == "split":
+                wt = _lib.packed_conv1x1_weight(weight, O, C, "split")   # hi/lo f16 fragments, once per weight
+                corr = self(coords)
+                _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
+                    corr.data_ptr(), B, C, H * W, wt.data_ptr(), bptr, O, out.data_ptr(), st),
+                    "CorrBlock lookup+conv1x1+relu (split)")
+            else:
+                wt = _lib.packed_conv1x1_weight(weight, O, C)   # MFMA fragment order, re-laid once per weight
+                _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu_packed(
+                    self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, self.num_levels,
+                    self.radius, wt.data_ptr(), bptr, O, out.data_ptr(), st), "CorrBlock lookup+conv1x1+relu")
         return out
 
     @staticmethod

@@ -240,6 +240,23 @@ ECORR_EXPORT int ecorr_lookup_conv1x1_relu_packed(const float* pyramid, const fl
     return launch_lookup_conv(P, B, packed, bias, O, out, (hipStream_t)stream, true);
 }
 
+ECORR_EXPORT int ecorr_conv1x1_split_size(int O, int C, int64_t* bytes) {
+    if (!bytes || O <= 0 || C <= 0) return ECORR_EINVAL;
+    *bytes = conv1x1_split_bytes(O, C);
+    return ECORR_OK;
+}
+
+ECORR_EXPORT int ecorr_conv1x1_split_pack(const float* weight, int O, int C, void* packed, void* stream) {
+    if (!weight || !packed) return ECORR_EINVAL;
+    return launch_conv1x1_split_pack(weight, O, C, packed, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_conv1x1_relu_split(const float* in, int B, int C, int Q, const void* packed,
+                                          const float* bias, int O, float* out, void* stream) {
+    if (!in || !packed || !out) return ECORR_EINVAL;
+    return launch_conv1x1_relu_split(in, B, C, Q, packed, bias, O, out, (hipStream_t)stream);
+}
+
 ECORR_EXPORT int ecorr_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,
                                         int Hg, int Wg, float* out, float* mask, void* stream) {
     if (!img || !coords || !out || N <= 0 || C < 0 || h <= 0 || w <= 0 || Hg <= 0 || Wg <= 0)

@@ -1,0 +1,263 @@
+// conv.hip -- SURVEY §8f row 1, two-launch form: relu(convc1(corr)) (update.py:67,74:
+// cor = F.relu(self.convc1(corr))) on the lookup's NCHW output, as a split-f16 MFMA GEMM:
+//
+//   out[b][o][p] = relu(bias[o] + sum_c W[o][c] * corr[b][c][p])
+//
+// The fused kernels (motion.hip) keep the 324-channel tile in LDS but pay for it in occupancy: their
+// gather runs on 4 waves per CU where the standalone lookup keeps 15 in flight, and the fp32 MFMA GEMM
+// is 16x slower per flop than f16.  Here the lookup writes corr (99.5 MB at DSEC B=16) and this kernel
+// reads it back, with the f16 matrix cores doing the channel sum:
+//
+//   split arithmetic (as the build, build.hip pack_body): every query column p of corr is scaled by
+//   2^e_p (its largest |value| over the C channels in [2^14, 2^15)), every weight row o by 2^e_o, and
+//   each scaled value x is split into hi = f16(x), lo = f16(x - hi) (exact subtraction), so
+//   x = hi + lo + O(2^-22 |x|); each product is lo.hi + hi.lo + hi.hi on v_mfma_f32_32x32x16_f16
+//   with fp32 accumulation, scaled back by 2^-(e_o + e_p) (v_ldexp, exact), then + bias, ReLU.
+//   Normwise within 1e-5 of an fp64 conv (tests/test_conv_split_gpu.py); NaN propagates to the
+//   query's outputs as in the reference; a +-inf corr or weight value gives NaN (inf - inf in the
+//   split), where the reference's fp32 conv can give +-inf -- the build's split mode has the same
+//   deviation, and the split build never produces inf samples.
+//
+// Workgroup = 64 queries x 256 output channels, 4 waves: wave w owns query block qb = w & 1 (32
+// queries: the MFMA's N) and channel half oh = w >> 1 (4 x 32 channels: M), 4 accumulator tiles.
+//   pre-pass  per query the max |corr| over C (each wave half of the chunks, lanes = queries,
+//             combined through LDS) -> e_p;
+//   K loop    per 16-channel chunk: the weight chunk (16 KB, the A fragments of all 8 channel
+//             blocks, hi and lo, pre-split and laid out in fragment order by ecorr_conv1x1_split_pack)
+//             goes global -> registers -> LDS one chunk ahead, double-buffered, one barrier per chunk;
+//             the B fragment (lane = query, 8 consecutive channels) is loaded from corr as 8 dwords
+//             two chunks ahead, split in registers; 4 x 3 MFMAs per wave.
+// Work: 2*O*C flop per query (12.7 GFLOP at DSEC B=16) as 3 f16 MFMAs per product; bytes: corr in
+// (C*4 per query, read twice: the max pre-pass and the K loop) + out (O*4 per query).
+
+#include "ecorr_device.h"
+#include "ecorr_internal.h"
+
+#include <algorithm>
+
+namespace ecorr {
+
+namespace {
+
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef unsigned int uintx4 __attribute__((ext_vector_type(4)));
+
+constexpr int SQ = 64;                 // queries per workgroup
+constexpr int SO = 256;                // output channels per workgroup (8 row blocks of 32)
+constexpr int SNT = 256;               // threads (4 waves)
+constexpr int SKC = 16;                // channels per chunk (one v_mfma_f32_32x32x16_f16 K)
+constexpr int SCHUNK = 8 * 2 * 64 * 16;   // bytes per packed weight chunk: [row block][hi | lo][lane][16 B]
+
+__host__ __device__ constexpr int split_chunks(int C) { return (C + SKC - 1) / SKC; }
+__host__ __device__ constexpr int split_oblocks(int O) { return (O + SO - 1) / SO; }
+
+__device__ __forceinline__ float pow2(int e) { return __int_as_float((e + 127) << 23); }
+
+// e such that m 2^e lies in [2^14, 2^15); 0 for a zero or non-finite maximum (build.hip pack_body)
+__device__ __forceinline__ int split_exponent(float m) {
+    int E = 0;
+    frexpf(m, &E);
+    const int e = (m > 0.f && m <= 3.4028235e38f) ? 15 - E : 0;
+    return e < -126 ? -126 : (e > 126 ? 126 : e);
+}
+
+__device__ __forceinline__ void split8(const float (&v)[8], float s, halfx8& hi, halfx8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = v[j] * s;
+        const _Float16 h = (_Float16)x;
+        hi[j] = h;
+        lo[j] = (_Float16)(x - (float)h);
+    }
+}
+
+// Packed weight: for output block ob (256 channels) and chunk c, 16 KB at (ob nkc + c) SCHUNK:
+// [row block rb][hi | lo][lane l][8 halves] = W[256 ob + 32 rb + (l & 31)][16 c + 8 (l >> 5) + j]
+// scaled by 2^e_o and split (zeros past O or C) -- the v_mfma_f32_32x32x16_f16 A fragment of lane l;
+// then the int exponents e_o of all nob * 256 rows.  One workgroup per output block.
+__global__ __launch_bounds__(SNT) void split_pack_kernel(const float* __restrict__ wt, int O, int C,
+                                                         char* __restrict__ packed) {
+    __shared__ float sc[SO];
+    const int ob = blockIdx.x, nob = gridDim.x, nkc = split_chunks(C), t = threadIdx.x;
+    const int o = ob * SO + t;
+    float m = 0.f;
+    if (o < O)
+        for (int k = 0; k < C; ++k) m = fmaxf(m, fabsf(wt[(int64_t)o * C + k]));
+    const int e = split_exponent(m);
+    sc[t] = pow2(e);
+    reinterpret_cast<int*>(packed + (int64_t)nob * nkc * SCHUNK)[o] = e;
+    __syncthreads();
+    char* base = packed + (int64_t)ob * nkc * SCHUNK;
+    for (int i = t; i < nkc * (SCHUNK / 16); i += SNT) {
+        const int l = i & 63, part = (i >> 6) & 1, rb = (i >> 7) & 7, c = i >> 10;
+        const int r = rb * 32 + (l & 31), oo = ob * SO + r, k0 = c * SKC + 8 * (l >> 5);
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (oo < O && k0 + j < C) ? wt[(int64_t)oo * C + k0 + j] : 0.f;
+        halfx8 hi, lo;
+        split8(v, sc[r], hi, lo);
+        *reinterpret_cast<halfx8*>(base + (int64_t)i * 16) = part ? lo : hi;
+    }
+}
+
+__global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restrict__ in, int C, int Q,
+                                                            const char* __restrict__ packed,
+                                                            const float* __restrict__ bias, int O,
+                                                            float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char wbuf[2][SCHUNK];
+    __shared__ float red[2][SQ];
+    __shared__ __attribute__((aligned(16))) int sex[SO];      // the block's weight-row exponents
+    __shared__ __attribute__((aligned(16))) float sbias[SO];  // and biases (0 past O or without bias)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, qb = w & 1, oh = w >> 1;
+    const int ob = blockIdx.y, b = blockIdx.z, nob = gridDim.y, nkc = split_chunks(C);
+    const int qi = 32 * qb + (lane & 31), q = blockIdx.x * SQ + qi, kh = lane >> 5;
+    const bool qok = q < Q;
+    // corr / out of batch item b as range-checked buffers: a lane past Q starts at the end of the
+    // range (every access then reads 0 / is dropped), channels past C or O fall outside by
+    // themselves -- no branches around the loads and stores
+    const __amdgpu_buffer_rsrc_t csrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(in + (int64_t)b * C * Q), 0, C * Q * 4, 0x00020000);
+    const int cbase = (qok ? q : C * Q) * 4, qs = Q * 4;
+    const char* wsrc = packed + (int64_t)ob * nkc * SCHUNK;
+
+    // B fragment of chunk c: corr[b][16 c + 8 kh + j][q], j = 0..7 (zeros past C or Q)
+    auto load_b = [&](int c, float (&v)[8]) __attribute__((always_inline)) {
+        const int off = cbase + (c * SKC + 8 * kh) * qs;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, off + j * qs, 0, 0));
+    };
+
+    {
+        const int o = ob * SO + tid;
+        sex[tid] = reinterpret_cast<const int*>(packed + (int64_t)nob * nkc * SCHUNK)[o];
+        sbias[tid] = (bias && o < O) ? bias[o] : 0.f;
+    }
+
+    // ---- pre-pass: the query's largest |value| over C -> its exponent
+    float m = 0.f;
+#pragma unroll 1
+    for (int c = oh; c < nkc; c += 8) {   // 4 chunks' loads in flight at once (clamped repeats past C)
+        float v[4][8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) load_b(min(c + 2 * k, nkc - 1), v[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[k][j]));
+    }
+    m = fmaxf(m, __shfl_xor(m, 32));
+    if (kh == 0) red[oh][qi] = m;
+
+    uintx4 wr[4];
+    auto load_w = [&](int c) __attribute__((always_inline)) {
+        const uintx4* p = reinterpret_cast<const uintx4*>(wsrc + (int64_t)c * SCHUNK);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wr[i] = p[tid + SNT * i];
+    };
+    auto store_w = [&](int buf) __attribute__((always_inline)) {
+        uintx4* p = reinterpret_cast<uintx4*>(wbuf[buf]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p[tid + SNT * i] = wr[i];
+    };
+    load_w(0);
+    store_w(0);
+    load_w(nkc > 1 ? 1 : 0);
+    float bv[3][8];   // B values of chunks c, c + 1, c + 2 (three fixed register sets: no copies)
+    load_b(0, bv[0]);
+    load_b(1, bv[1]);   // past C: out of range, zeros
+    __syncthreads();
+    const int eq = split_exponent(fmaxf(red[0][qi], red[1][qi]));
+    const float sq = pow2(eq);
+
+    floatx16 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+    // ---- K loop: chunk c's weights in wbuf[c & 1] (published by the barrier before); its B values
+    // in set cur, and chunk c + 2's loads go to set nxt (chunk c - 1's, consumed)
+    auto step = [&](int c, float (&cur)[8], float (&nxt)[8]) __attribute__((always_inline)) {
+        load_b(c + 2, nxt);   // unconditional (past C reads zeros): no branch for the waits to merge over
+        __builtin_amdgcn_sched_barrier(0);   // issued here, ahead of this chunk's work
+        halfx8 bh, bl;
+        split8(cur, sq, bh, bl);
+        const char* wb = wbuf[c & 1] + lane * 16;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int rb = 4 * oh + i;
+            const halfx8 ah = *reinterpret_cast<const halfx8*>(wb + (rb * 2 + 0) * 1024);
+            const halfx8 al = *reinterpret_cast<const halfx8*>(wb + (rb * 2 + 1) * 1024);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[i], 0, 0, 0);
+        }
+        store_w((c + 1) & 1);   // its readers (chunk c - 1) passed the last barrier; past the
+        load_w(min(c + 2, nkc - 1));   // last chunk a harmless repeat
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+    };
+    int c = 0;
+#pragma unroll 1
+    for (; c + 3 <= nkc; c += 3) {
+        step(c, bv[0], bv[2]);
+        step(c + 1, bv[1], bv[0]);
+        step(c + 2, bv[2], bv[1]);
+    }
+    if (c < nkc) step(c, bv[0], bv[2]);
+    if (c + 1 < nkc) step(c + 1, bv[1], bv[0]);
+
+    // ---- epilogue: lane holds query q, channels 32 rb + 8 (r >> 2) + 4 kh + (r & 3)
+    const __amdgpu_buffer_rsrc_t osrc = __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)b * O * Q, 0, O * Q * 4,
+                                                                          0x00020000);
+    const int obase = (qok ? q : O * Q) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int ol = 32 * (4 * oh + i) + 8 * g + 4 * kh;   // 4 consecutive channels r & 3
+            const int4 eo = *reinterpret_cast<const int4*>(&sex[ol]);
+            const float4 bo = *reinterpret_cast<const float4*>(&sbias[ol]);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                float v = ldexpf(acc[i][4 * g + t], -(eo[t] + eq));
+                v = v + bo[t];   // a missing bias is 0 (v + 0 = v for every v but -0, which ReLU maps to 0)
+                v = v < 0.f ? 0.f : v;   // torch.relu: NaN stays NaN
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), osrc, obase + (ob * SO + ol + t) * qs, 0,
+                                                      0);
+            }
+        }
+}
+
+}  // namespace
+
+int64_t conv1x1_split_bytes(int O, int C) {
+    return (int64_t)split_oblocks(O) * split_chunks(C) * SCHUNK + (int64_t)split_oblocks(O) * SO * 4;
+}
+
+int launch_conv1x1_split_pack(const float* wt, int O, int C, void* packed, hipStream_t stream) {
+    if (O <= 0 || C <= 0 || split_oblocks(O) > 65535) return ECORR_EINVAL;
+    hipLaunchKernelGGL(split_pack_kernel, dim3(split_oblocks(O)), dim3(SNT), 0, stream, wt, O, C, (char*)packed);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
+}
+
+int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const void* packed, const float* bias, int O,
+                              float* out, hipStream_t stream) {
+    if (B <= 0 || C <= 0 || Q <= 0 || O <= 0 || B > 65535 || split_oblocks(O) > 65535) return ECORR_EINVAL;
+    // 32-bit buffer offsets: a lane past Q reads from C*Q on, the prefetch reaches 3 chunks past C; the stores
+    // likewise from O*Q up to the output block's last row
+    if ((int64_t)(2 * C + 4 * SKC) * Q * 4 >= 0x7fffffffLL ||
+        (int64_t)(O + split_oblocks(O) * SO) * Q * 4 >= 0x7fffffffLL)
+        return ECORR_EINVAL;
+    if ((const void*)in == (const void*)out) return ECORR_EINVAL;
+    const dim3 grid((unsigned)((Q + SQ - 1) / SQ), (unsigned)split_oblocks(O), (unsigned)B);
+    hipLaunchKernelGGL(conv1x1_split_kernel, grid, dim3(SNT), 0, stream, in, C, Q, (const char*)packed, bias, O,
+                       out);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
+}
+
+}  // namespace ecorr

@@ -71,6 +71,11 @@ int launch_lookup_conv(const LookupParams& P, int B, const float* wt, const floa
                        hipStream_t stream, bool packed);
 int64_t conv1x1_packed_floats(int O, int C);
 int launch_conv1x1_pack(const float* wt, int O, int C, float* packed, hipStream_t stream);
+// conv.hip: split-f16 1x1 conv + ReLU on an NCHW tensor (ecorr_conv1x1_relu_split)
+int64_t conv1x1_split_bytes(int O, int C);
+int launch_conv1x1_split_pack(const float* wt, int O, int C, void* packed, hipStream_t stream);
+int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const void* packed, const float* bias, int O,
+                              float* out, hipStream_t stream);
 
 int launch_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,
                             int Hg, int Wg, float* out, float* mask, hipStream_t stream);

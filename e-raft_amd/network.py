@@ -183,8 +183,8 @@ class ImagePadder:
 class ERAFT(nn.Module):
     """E-RAFT with the MI355X CorrBlock (eraft.py:37-145).  config needs 'subtype' in
     {'standard', 'warm_start'}; n_first_channels = voxel bins.  fuse_motion_corr=True replaces
-    `corr_fn(coords1)` + BasicMotionEncoder's `relu(convc1(corr))` with the fused HIP kernel
-    (CorrBlock.lookup_conv1x1_relu); hip_upsample=True runs upsample_flow as
+    `corr_fn(coords1)` + BasicMotionEncoder's `relu(convc1(corr))` with the HIP lookup + convc1
+    (CorrBlock.lookup_conv1x1_relu; its ECORR_CONVC1 mode); hip_upsample=True runs upsample_flow as
     the one-pass HIP kernel (eraft_amd.upsample_flow).  The defaults keep the
     reference's call pattern exactly."""
 

@@ -20,6 +20,8 @@ collective lands in a persistent receive buffer [world][chunk], and one HIP kern
 collective is RCCL over xGMI with the "nccl" backend (all_gather_into_tensor); any other backend
 (the CPU tests use gloo) gets all_gather into views of the same receive buffer.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -239,10 +241,13 @@ class RowShardedCorrBlock:
         self._lookup_into(coords_rows, self._ex.send_slab(B, C, W, device=self._device))
         return self._ex.gather(B, C, W, self._device)                        # exchange 2
 
-    def lookup_conv1x1_relu(self, coords, weight, bias=None):
+    def lookup_conv1x1_relu(self, coords, weight, bias=None, mode=None):
         """F.relu(conv1x1(self(coords), weight, bias)) for the full map on every rank: this rank's
-        rows through the fused lookup + convc1 + ReLU kernel (CorrBlock.lookup_conv1x1_relu), then
+        rows through the lookup + convc1 + ReLU (CorrBlock.lookup_conv1x1_relu, same `mode`), then
         the O-channel all-gather (exchange 2, fused form)."""
+        mode = mode or os.environ.get("ECORR_CONVC1", "split")
+        if mode not in ("split", "fused"):
+            raise ValueError(f"mode {mode!r}: expected 'split' or 'fused'")
         B, _, H, W = self._shape
         coords_rows = self._full_coords_rows(coords)
         _require_device_f32("weight", weight)
@@ -259,13 +264,21 @@ class RowShardedCorrBlock:
             if bias.numel() != O:
                 raise RuntimeError(f"bias has {bias.numel()} elements, expected {O}")
             bias = bias.contiguous()
-        if O <= 0 or O % 64 != 0:
+        if mode == "fused" and (O <= 0 or O % 64 != 0):
             raise RuntimeError(f"{O} output channels: the fused kernel needs a positive multiple of 64")
         if self.world == 1:
             out = torch.empty((B, O, H, W), dtype=torch.float32, device=self._device)
         else:
             out = self._ex.send_slab(B, O, W, device=self._device)
         with _lib.on_device(self._device):
+            if mode == "split":
+                wt = _lib.packed_conv1x1_weight(weight, O, C, "split")
+                corr = torch.empty((B, C, self.q_count), dtype=torch.float32, device=self._device)
+                self._lookup_into(coords_rows, corr)
+                _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
+                    corr.data_ptr(), B, C, self.q_count, wt.data_ptr(), None if bias is None else bias.data_ptr(),
+                    O, out.data_ptr(), _lib.stream_of(out)), "RowShardedCorrBlock lookup+conv1x1+relu (split)")
+                return out if self.world == 1 else self._ex.gather(B, O, W, self._device)
             wt = _lib.packed_conv1x1_weight(weight, O, C)   # MFMA fragment order, re-laid once per weight
             _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu_packed(
                 self._pyramid.data_ptr(), coords_rows.data_ptr(), B, H, W, self.q_count, self.num_levels,

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 14
+#define ECORR_ABI_VERSION 15
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -129,6 +129,21 @@ int ecorr_conv1x1_pack(const float* weight, int O, int C, float* packed, void* s
 int ecorr_lookup_conv1x1_relu_packed(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
                                      int levels, int radius, const float* packed, const float* bias, int O,
                                      float* out, void* stream);
+
+/* convc1 + ReLU on a materialized lookup (ABI 15; SURVEY §8f row 1 as two launches: ecorr_lookup,
+ * then this): out float[B][O][Q] = relu(bias[o] + sum_c weight[o][c] * in[b][c][p]) for any
+ * in float[B][C][Q] (the lookup's [B][C][H][W] with Q = H*W or a q_count slab), on the f16 matrix
+ * cores with split operands (each fp32 value as hi + lo f16 under a per-query / per-output-row
+ * power-of-two scale; three MFMAs per product): normwise within 1e-5 of the fp32 conv, not bitwise.
+ * ecorr_conv1x1_split_size gives the packed weight's byte count, ecorr_conv1x1_split_pack writes it
+ * from weight float[O][C] (stream-ordered); valid until the weight changes.  bias float[O] or NULL;
+ * in and out must not overlap (ECORR_EINVAL when they are the same pointer, or when the 32-bit
+ * buffer offsets, about (2C + 64) * Q * 4 bytes, would overflow).
+ * Replaces: F.relu(self.convc1(corr)) (update.py:67,74). */
+int ecorr_conv1x1_split_size(int O, int C, int64_t* bytes);
+int ecorr_conv1x1_split_pack(const float* weight, int O, int C, void* packed, void* stream);
+int ecorr_conv1x1_relu_split(const float* in, int B, int C, int Q, const void* packed, const float* bias, int O,
+                             float* out, void* stream);
 
 /* Generic bilinear_sampler: img float[N][C][h][w], coords float[N][Hg][Wg][2] in pixels ->
  * out float[N][C][Hg][Wg]; mask (nullable) float[N][Hg][Wg] = 1 where the normalized sample

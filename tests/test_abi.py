@@ -119,6 +119,20 @@ def test_argument_validation_before_launch(ea):
     assert L.ecorr_conv1x1_packed_size(96, 324, ctypes.byref(n)) == _lib.ECORR_EINVAL
     assert L.ecorr_conv1x1_pack(None, 256, 324, 8, None) == _lib.ECORR_EINVAL
     assert L.ecorr_conv1x1_pack(8, 100, 324, 8, None) == _lib.ECORR_EINVAL
+    # split-f16 convc1 + ReLU (ABI 15): [O/256 blocks][ceil(C/16) chunks][16 KB] + O-block exponents
+    assert L.ecorr_conv1x1_split_size(256, 324, ctypes.byref(n)) == _lib.ECORR_OK
+    assert n.value == 1 * 21 * 16384 + 256 * 4
+    assert L.ecorr_conv1x1_split_size(300, 324, ctypes.byref(n)) == _lib.ECORR_OK
+    assert n.value == 2 * 21 * 16384 + 512 * 4
+    assert L.ecorr_conv1x1_split_size(0, 324, ctypes.byref(n)) == _lib.ECORR_EINVAL
+    assert L.ecorr_conv1x1_split_pack(None, 256, 324, 8, None) == _lib.ECORR_EINVAL
+    assert L.ecorr_conv1x1_split_pack(8, 256, 0, 8, None) == _lib.ECORR_EINVAL
+    S = L.ecorr_conv1x1_relu_split   # (in, B, C, Q, packed, bias, O, out, stream)
+    assert S(None, 1, 324, 4800, 8, None, 256, 16, None) == _lib.ECORR_EINVAL
+    assert S(8, 1, 324, 4800, None, None, 256, 16, None) == _lib.ECORR_EINVAL
+    assert S(8, 0, 324, 4800, 8, None, 256, 16, None) == _lib.ECORR_EINVAL
+    assert S(8, 1, 324, 4800, 8, None, 256, 8, None) == _lib.ECORR_EINVAL   # in == out
+    assert S(8, 1, 324, 1 << 20, 8, None, 256, 16, None) == _lib.ECORR_EINVAL   # 32-bit offsets
     # the split build's stages validate like the whole call (no workspace / no operands)
     assert L.ecorr_build_split_pack(8, 8, 1, 256, 8, 8, 64, None, None) == _lib.ECORR_EINVAL
     assert L.ecorr_build_split_pack(None, 8, 1, 256, 8, 8, 64, 256, None) == _lib.ECORR_EINVAL

@@ -1,0 +1,127 @@
+"""GPU parity of the split-f16 convc1 + ReLU (ecorr_conv1x1_relu_split, conv.hip; SURVEY §8f row 1's
+default mode) on arbitrary NCHW inputs, against an fp64 conv of the same fp32 input.
+
+Bar (north star: the conv is floating point, normwise): max|got - ref| / rms(ref) <= 1e-5 over
+the outputs, for inputs whose per-query scales span 2^-40..2^40, all-zero query columns, weight
+rows at different scales, ragged Q (not a multiple of the 64-query tile) and O (not a multiple of
+the 256-channel tile), C = 81 / 243 / 324, with and without bias.  NaN in a query's column makes
+exactly that query's outputs NaN (as the reference's conv: NaN * w propagates, relu(NaN) = NaN).
+"""
+import numpy as np
+import pytest
+import torch
+
+import prng
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def ea():
+    if not torch.cuda.is_available():
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    import eraft_amd
+    eraft_amd.lib()
+    return eraft_amd
+
+
+def _conv_split(x, w, bias):
+    from eraft_amd import _lib
+    B, C, Q = x.shape
+    O = w.shape[0]
+    pk = _lib.packed_conv1x1_weight(w, O, C, "split")
+    out = torch.empty((B, O, Q), dtype=torch.float32, device=DEV)
+    _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
+        x.data_ptr(), B, C, Q, pk.data_ptr(), None if bias is None else bias.data_ptr(), O, out.data_ptr(),
+        _lib.stream_of(x)), "split conv")
+    torch.cuda.synchronize()
+    return out
+
+
+def _ref(x, w, bias):
+    r = torch.einsum("oc,bcq->boq", w.double().cpu(), x.double().cpu())
+    if bias is not None:
+        r = r + bias.double().cpu().view(1, -1, 1)
+    return torch.relu(r).numpy()
+
+
+def _normwise(got, ref):
+    return float(np.max(np.abs(got.cpu().numpy().astype(np.float64) - ref)) / np.sqrt(np.mean(ref * ref)))
+
+
+@pytest.mark.parametrize("shape", [(2, 324, 4800, 256), (1, 324, 100, 256), (3, 243, 130, 96),
+                                   (1, 81, 64, 300), (2, 324, 1, 256)],
+                         ids=lambda s: "b%d_c%d_q%d_o%d" % s)
+@pytest.mark.parametrize("with_bias", [True, False], ids=["bias", "nobias"])
+def test_dense_normwise(ea, shape, with_bias):
+    B, C, Q, O = shape
+    x = torch.from_numpy(prng.normal(201, (B, C, Q))).to(DEV)
+    w = torch.from_numpy(prng.normal(202, (O, C)) * np.float32(0.05)).to(DEV)
+    bias = torch.from_numpy(prng.normal(203, (O,)) * np.float32(0.1)).to(DEV) if with_bias else None
+    with torch.no_grad():
+        got = _conv_split(x, w, bias)
+    assert _normwise(got, _ref(x, w, bias)) <= 1e-5
+
+
+def test_scales_and_zero_columns(ea):
+    """Per-query scales 2^-40..2^40 and weight rows 2^-20..2^20: each query column and weight row
+    gets its own power-of-two exponent, so each output (o, q) keeps the split's 2^-22 relative error
+    of its own products; zero columns stay exactly 0 after ReLU (+ zero bias)."""
+    B, C, Q, O = 2, 324, 700, 256
+    x = prng.normal(211, (B, C, Q))
+    qs = np.exp2(np.linspace(-40, 40, Q)).astype(np.float32)
+    x = (x * qs[None, None, :]).astype(np.float32)
+    x[:, :, 5] = 0.0
+    w = prng.normal(212, (O, C)).astype(np.float32)
+    ws = np.exp2(np.linspace(-20, 20, O)).astype(np.float32)
+    w = (w * ws[:, None]).astype(np.float32)
+    xt, wt = torch.from_numpy(x).to(DEV), torch.from_numpy(w).to(DEV)
+    with torch.no_grad():
+        got = _conv_split(xt, wt, None).cpu().numpy().astype(np.float64)
+    ref = _ref(xt, wt, None)
+    assert np.all(got[:, :, 5] == 0.0)
+    # per (o, q) relative to that output's own scale: |W[o]| . |x[:, q]|
+    scale = np.einsum("oc,bcq->boq", np.abs(w.astype(np.float64)), np.abs(x.astype(np.float64)))
+    rel = np.abs(got - ref) / np.maximum(scale, 1e-300)
+    assert rel.max() <= 1e-5, rel.max()
+
+
+def test_nan_column_propagates(ea):
+    B, C, Q, O = 1, 324, 200, 256
+    x = prng.normal(221, (B, C, Q))
+    x[0, 17, 33] = np.nan
+    w = (prng.normal(222, (O, C)) * np.float32(0.05)).astype(np.float32)
+    xt, wt = torch.from_numpy(x).to(DEV), torch.from_numpy(w).to(DEV)
+    with torch.no_grad():
+        got = _conv_split(xt, wt, None).cpu().numpy()
+    assert np.all(np.isnan(got[0, :, 33]))
+    keep = np.ones(Q, bool)
+    keep[33] = False
+    assert np.all(np.isfinite(got[0][:, keep]))
+    x2 = x.copy()
+    x2[0, :, 33] = 0.0
+    ref = _ref(torch.from_numpy(x2), torch.from_numpy(w), None)
+    assert _normwise(torch.from_numpy(got[:, :, keep]), ref[:, :, keep]) <= 1e-5
+
+
+def test_weight_repack_on_update(ea):
+    """The packed split weight is cached per weight tensor and re-made after an in-place update."""
+    B, C, Q, O = 1, 324, 256, 256
+    x = torch.from_numpy(prng.normal(231, (B, C, Q))).to(DEV)
+    w = torch.from_numpy(prng.normal(232, (O, C)) * np.float32(0.05)).to(DEV)
+    with torch.no_grad():
+        a = _conv_split(x, w, None)
+        w.mul_(-1.0)
+        b = _conv_split(x, w, None)
+    assert _normwise(b, _ref(x, w, None)) <= 1e-5
+    assert not torch.equal(a, b)
+
+
+def test_in_out_alias_rejected(ea):
+    from eraft_amd import _lib
+    x = torch.zeros((1, 324, 64), device=DEV)
+    w = torch.zeros((256, 324), device=DEV)
+    pk = _lib.packed_conv1x1_weight(w, 256, 324, "split")
+    assert _lib.lib().ecorr_conv1x1_relu_split(x.data_ptr(), 1, 324, 64, pk.data_ptr(), None, 256, x.data_ptr(),
+                                               _lib.stream_of(x)) == _lib.ECORR_EINVAL

@@ -1,10 +1,12 @@
-"""GPU parity of the fused lookup + convc1 + ReLU kernel (SURVEY §8f row 1,
-CorrBlock.lookup_conv1x1_relu -> ecorr_lookup_conv1x1_relu) against the unfused path.
+"""GPU parity of lookup + convc1 + ReLU (CorrBlock.lookup_conv1x1_relu) in both
+modes: "fused" (ecorr_lookup_conv1x1_relu[_packed], one kernel, fp32 MFMA) and "split" (the
+default: ecorr_lookup, then ecorr_conv1x1_relu_split on the f16 matrix cores) against the unfused
+path.  Split-mode specifics (scales, NaN, ragged O / Q): test_conv_split_gpu.py.
 
 Bars: with one-hot weights (each output channel copies one correlation channel, times 1, plus a
-bias) the fused output is BIT-EXACT relu(corr + bias), because an fmaf chain over exact zeros and
+bias) the fused-mode output is BIT-EXACT relu(corr + bias), because an fmaf chain over exact zeros and
 one exact 1.0 reproduces its input -- this pins the sampling, the channel order and the epilogue;
-with dense weights the output agrees normwise (max|d| / rms <= 1e-5) with an fp64 conv of our own
+with dense weights either mode's output agrees normwise (max|d| / rms <= 1e-5) with an fp64 conv of our own
 (bit-exact, oracle-checked) lookup output; e2e flow with the fused path stays within the 1e-3 px
 EPE bar of the reference goldens (test_e2e_gpu.py cases).
 """
@@ -52,17 +54,18 @@ def test_one_hot_weights_bit_exact(ea, shape):
         wgt = torch.zeros(O, C, 1, 1, device=DEV)
         wgt[torch.arange(O), pick] = 1.0
         bias = torch.from_numpy(prng.normal(33, (O,))).to(DEV)
-        out = blk.lookup_conv1x1_relu(coords, wgt, bias)
+        out = blk.lookup_conv1x1_relu(coords, wgt, bias, mode="fused")
         ref = torch.relu(corr[:, pick] + bias.view(1, O, 1, 1))
     assert oracle.same_bits(out.cpu().numpy(), ref.cpu().numpy())
     # no bias: pure copy through relu
     with torch.no_grad():
-        out0 = blk.lookup_conv1x1_relu(coords, wgt[:, :, 0, 0])
+        out0 = blk.lookup_conv1x1_relu(coords, wgt[:, :, 0, 0], mode="fused")
     assert oracle.same_bits(out0.cpu().numpy(), torch.relu(corr[:, pick]).cpu().numpy())
 
 
+@pytest.mark.parametrize("mode", ["fused", "split"])
 @pytest.mark.parametrize("shape", [(2, 64, 16, 24), (16, 256, 60, 80)], ids=["small", "dsec_b16"])
-def test_dense_weights_normwise(ea, shape):
+def test_dense_weights_normwise(ea, shape, mode):
     B, D, H, W = shape
     with torch.no_grad():
         blk = _block(ea, B, D, H, W, 41)
@@ -71,7 +74,7 @@ def test_dense_weights_normwise(ea, shape):
         corr = blk(coords)
         wgt = torch.from_numpy(prng.normal(43, (256, 324, 1, 1)) * 0.05).to(DEV)
         bias = torch.from_numpy(prng.normal(44, (256,)) * 0.1).to(DEV)
-        out = blk.lookup_conv1x1_relu(coords, wgt, bias)
+        out = blk.lookup_conv1x1_relu(coords, wgt, bias, mode=mode)
     # our lookup is bit-exact vs the oracle (checked elsewhere); conv it in fp64 here
     c64 = corr.double().cpu()
     ref = torch.relu(torch.einsum("oc,bchw->bohw", wgt[:, :, 0, 0].double().cpu(), c64)
@@ -88,8 +91,12 @@ def test_fused_rejects_unsupported(ea):
     with torch.no_grad():
         blk = ea.CorrBlock(torch.zeros(1, 8, 16, 16, device=DEV), torch.zeros(1, 8, 16, 16, device=DEV),
                            radius=3)
+        with pytest.raises(ValueError):   # the fused kernel is radius 4 only
+            blk.lookup_conv1x1_relu(torch.zeros(1, 2, 16, 16, device=DEV), torch.zeros(64, 196, device=DEV),
+                                    mode="fused")
         with pytest.raises(ValueError):
-            blk.lookup_conv1x1_relu(torch.zeros(1, 2, 16, 16, device=DEV), torch.zeros(64, 196, device=DEV))
+            blk.lookup_conv1x1_relu(torch.zeros(1, 2, 16, 16, device=DEV), torch.zeros(64, 196, device=DEV),
+                                    mode="fp32")
         blk = ea.CorrBlock(torch.zeros(1, 8, 16, 16, device=DEV), torch.zeros(1, 8, 16, 16, device=DEV))
         with pytest.raises(RuntimeError):   # weight does not map 324 channels
             blk.lookup_conv1x1_relu(torch.zeros(1, 2, 16, 16, device=DEV), torch.zeros(64, 300, device=DEV))
@@ -107,7 +114,7 @@ def test_packed_weight_matches_weight_as_stored(ea, shape):
         coords = torch.from_numpy(prng.coords_with_flow(52, B, H, W, 3.0)).to(DEV)
         wgt = torch.from_numpy(prng.normal(53, (O, C, 1, 1)) * 0.05).to(DEV)
         bias = torch.from_numpy(prng.normal(54, (O,)) * 0.1).to(DEV)
-        got = blk.lookup_conv1x1_relu(coords, wgt, bias)
+        got = blk.lookup_conv1x1_relu(coords, wgt, bias, mode="fused")
         ref = torch.empty_like(got)
         _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu(
             blk._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, L, 4, wgt.data_ptr(), bias.data_ptr(), O,
@@ -115,7 +122,7 @@ def test_packed_weight_matches_weight_as_stored(ea, shape):
         torch.cuda.synchronize()
         assert torch.equal(got, ref)
         wgt.mul_(-1.0)   # in place: the cached packed weight must not be reused
-        got2 = blk.lookup_conv1x1_relu(coords, wgt, bias)
+        got2 = blk.lookup_conv1x1_relu(coords, wgt, bias, mode="fused")
         _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu(
             blk._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, L, 4, wgt.data_ptr(), bias.data_ptr(), O,
             ref.data_ptr(), _lib.stream_of(coords)), "unpacked")

@@ -46,11 +46,12 @@ def _worker(rank, world, port, shape, q):
         with torch.no_grad():
             full = eraft_amd.CorrBlock(f1, f2)
             ref = full(coords)
-            ref_fused = full.lookup_conv1x1_relu(coords, wt, bias)
+            ref_fused = {m: full.lookup_conv1x1_relu(coords, wt, bias, mode=m) for m in ("fused", "split")}
             sh = RowShardedCorrBlock.from_row_slabs(f1[:, :, r0:r0 + rr], f2[:, :, r0:r0 + rr], H)
             for it in range(2):   # persistent exchange buffers, reused
                 res[f"plain{it}"] = bool(torch.equal(sh(coords), ref))
-                res[f"fused{it}"] = bool(torch.equal(sh.lookup_conv1x1_relu(coords, wt, bias), ref_fused))
+                for m in ("fused", "split"):   # both convc1 modes: bitwise the unsharded rows
+                    res[f"{m}{it}"] = bool(torch.equal(sh.lookup_conv1x1_relu(coords, wt, bias, mode=m), ref_fused[m]))
             res["local"] = bool(torch.equal(sh.lookup_local(coords[:, :, r0:r0 + rr].contiguous()),
                                             ref[:, :, r0:r0 + rr]))
             rep = RowShardedCorrBlock(f1, f2)   # replicated-fmap constructor

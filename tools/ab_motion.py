@@ -45,7 +45,7 @@ with torch.no_grad():
     bias = torch.randn((256,), generator=g, device="cuda") * 0.1
 
     def call(c):
-        return blk.lookup_conv1x1_relu(c, wgt, bias)
+        return blk.lookup_conv1x1_relu(c, wgt, bias, mode="fused")
 
     if not os.environ.get("AB_NOCHECK"):
         ref = call(coords[0])
