@@ -101,14 +101,34 @@ __global__ __launch_bounds__(SNT) void split_pack_kernel(const float* __restrict
     }
 }
 
+// s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt bits 3:0 and 15:14; expcnt, lgkmcnt not waited)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt field");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// DMA: the weight chunks go global -> LDS by LDS-DMA (no staging registers), three buffers, two
+// chunks ahead, with static vmcnt waits; else through registers, two buffers, one chunk ahead.
+template <bool DMA>
 __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restrict__ in, int C, int Q,
                                                             const char* __restrict__ packed,
                                                             const float* __restrict__ bias, int O,
                                                             float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) char wbuf[2][SCHUNK];
-    __shared__ float red[2][SQ];
-    __shared__ __attribute__((aligned(16))) int sex[SO];      // the block's weight-row exponents
-    __shared__ __attribute__((aligned(16))) float sbias[SO];  // and biases (0 past O or without bias)
+    constexpr int NB = DMA ? 3 : 2;
+    // ALL LDS in one object: with a second __shared__ object hipcc waits vmcnt(0) before every
+    // ds_read while an LDS-DMA is in flight (cdna_hip_programming.md, the second-__shared__ trap)
+    struct Lds {
+        char wbuf[NB][SCHUNK];   // weight chunks
+        float red[2][SQ];        // per-query maxima of the two channel halves
+        int sex[SO];             // the block's weight-row exponents
+        float sbias[SO];         // and biases (0 past O or without bias)
+    };
+    __shared__ __attribute__((aligned(16))) Lds sh;
+    auto& wbuf = sh.wbuf;
+    auto& red = sh.red;
+    auto& sex = sh.sex;
+    auto& sbias = sh.sbias;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, qb = w & 1, oh = w >> 1;
     const int ob = blockIdx.y, b = blockIdx.z, nob = gridDim.y, nkc = split_chunks(C);
     const int qi = 32 * qb + (lane & 31), q = blockIdx.x * SQ + qi, kh = lane >> 5;
@@ -161,13 +181,36 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
 #pragma unroll
         for (int i = 0; i < 4; ++i) p[tid + SNT * i] = wr[i];
     };
-    load_w(0);
-    store_w(0);
-    load_w(nkc > 1 ? 1 : 0);
+    // DMA: wave w copies the chunk's 1-KB pieces w, w + 4, w + 8, w + 12 (lane-linear, as LDS-DMA
+    // writes them), the chunk offset in the scalar soffset
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wsrc), 0, nkc * SCHUNK, 0x00020000);
+    auto issue_w = [&](int c, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                wrs, (__attribute__((address_space(3))) void*)(wbuf[buf] + (w + 4 * s) * 1024), 16,
+                (w + 4 * s) * 1024 + lane * 16, c * SCHUNK, 0, 0);
+    };
     float bv[3][8];   // B values of chunks c, c + 1, c + 2 (three fixed register sets: no copies)
-    load_b(0, bv[0]);
-    load_b(1, bv[1]);   // past C: out of range, zeros
-    __syncthreads();
+    if constexpr (DMA) {
+        issue_w(0, 0);
+        issue_w(nkc > 1 ? 1 : 0, 1);
+        load_b(0, bv[0]);
+        load_b(1, bv[1]);   // past C: out of range, zeros
+        __builtin_amdgcn_sched_barrier(0);
+        wait_vm<20>();      // chunk 0's pieces (then chunk 1's 4 and 2 x 8 B loads may be in flight)
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): red / sex / sbias written
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    } else {
+        load_w(0);
+        store_w(0);
+        load_w(nkc > 1 ? 1 : 0);
+        load_b(0, bv[0]);
+        load_b(1, bv[1]);   // past C: out of range, zeros
+        __syncthreads();
+    }
     const int eq = split_exponent(fmaxf(red[0][qi], red[1][qi]));
     const float sq = pow2(eq);
 
@@ -179,12 +222,14 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
 
     // ---- K loop: chunk c's weights in wbuf[c & 1] (published by the barrier before); its B values
     // in set cur, and chunk c + 2's loads go to set nxt (chunk c - 1's, consumed)
-    auto step = [&](int c, float (&cur)[8], float (&nxt)[8]) __attribute__((always_inline)) {
+    // (DMA: chunk c in wbuf[c % 3], bufc; chunk c + 2 goes to bufn = (c + 2) % 3, chunk c - 1's)
+    auto step = [&](int c, float (&cur)[8], float (&nxt)[8], int bufc, int bufn) __attribute__((always_inline)) {
         load_b(c + 2, nxt);   // unconditional (past C reads zeros): no branch for the waits to merge over
+        if constexpr (DMA) issue_w(min(c + 2, nkc - 1), bufn);   // past the last chunk a harmless repeat
         __builtin_amdgcn_sched_barrier(0);   // issued here, ahead of this chunk's work
         halfx8 bh, bl;
         split8(cur, sq, bh, bl);
-        const char* wb = wbuf[c & 1] + lane * 16;
+        const char* wb = wbuf[DMA ? bufc : (c & 1)] + lane * 16;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int rb = 4 * oh + i;
@@ -194,20 +239,31 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
             acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[i], 0, 0, 0);
             acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[i], 0, 0, 0);
         }
-        store_w((c + 1) & 1);   // its readers (chunk c - 1) passed the last barrier; past the
-        load_w(min(c + 2, nkc - 1));   // last chunk a harmless repeat
-        __builtin_amdgcn_sched_barrier(0);
-        __syncthreads();
+        if constexpr (DMA) {
+            // chunk c + 1's pieces landed (only this step's 8 B loads + 4 pieces may be newer) and this
+            // wave's reads of chunk c are done (the next step's DMA overwrites it); a bare s_barrier:
+            // __syncthreads()'s release fence would wait for every load in flight (vmcnt(0))
+            __builtin_amdgcn_sched_barrier(0);
+            wait_vm<12>();
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            store_w((c + 1) & 1);   // its readers (chunk c - 1) passed the last barrier; past the
+            load_w(min(c + 2, nkc - 1));   // last chunk a harmless repeat
+            __builtin_amdgcn_sched_barrier(0);
+            __syncthreads();
+        }
     };
     int c = 0;
 #pragma unroll 1
     for (; c + 3 <= nkc; c += 3) {
-        step(c, bv[0], bv[2]);
-        step(c + 1, bv[1], bv[0]);
-        step(c + 2, bv[2], bv[1]);
+        step(c, bv[0], bv[2], 0, 2);
+        step(c + 1, bv[1], bv[0], 1, 0);
+        step(c + 2, bv[2], bv[1], 2, 1);
     }
-    if (c < nkc) step(c, bv[0], bv[2]);
-    if (c + 1 < nkc) step(c + 1, bv[1], bv[0]);
+    if (c < nkc) step(c, bv[0], bv[2], 0, 2);
+    if (c + 1 < nkc) step(c + 1, bv[1], bv[0], 1, 0);
 
     // ---- epilogue: lane holds query q, channels 32 rb + 8 (r >> 2) + 4 kh + (r & 3)
     const __amdgpu_buffer_rsrc_t osrc = __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)b * O * Q, 0, O * Q * 4,
@@ -230,6 +286,8 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
             }
         }
 }
+
+constexpr bool kConvDMA = true;
 
 }  // namespace
 
@@ -254,7 +312,7 @@ int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const void* 
         return ECORR_EINVAL;
     if ((const void*)in == (const void*)out) return ECORR_EINVAL;
     const dim3 grid((unsigned)((Q + SQ - 1) / SQ), (unsigned)split_oblocks(O), (unsigned)B);
-    hipLaunchKernelGGL(conv1x1_split_kernel, grid, dim3(SNT), 0, stream, in, C, Q, (const char*)packed, bias, O,
+    hipLaunchKernelGGL(conv1x1_split_kernel<kConvDMA>, grid, dim3(SNT), 0, stream, in, C, Q, (const char*)packed, bias, O,
                        out);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;

@@ -1012,6 +1012,10 @@ PATCHES["mo_wsst"] = [
 ]
 
 
+# split convc1 (conv.hip): weight chunks through registers instead of LDS-DMA
+PATCHES["cv_regw"] = [("conv.hip", "constexpr bool kConvDMA = true;", "constexpr bool kConvDMA = false;")]
+
+
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
     if os.path.exists(dst):
