@@ -223,7 +223,10 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
     // ---- K loop: chunk c's weights in wbuf[c & 1] (published by the barrier before); its B values
     // in set cur, and chunk c + 2's loads go to set nxt (chunk c - 1's, consumed)
     // (DMA: chunk c in wbuf[c % 3], bufc; chunk c + 2 goes to bufn = (c + 2) % 3, chunk c - 1's)
-    auto step = [&](int c, float (&cur)[8], float (&nxt)[8], int bufc, int bufn) __attribute__((always_inline)) {
+    // tail: a remainder step after the loop, whose query-column loads are dead (nothing reads that
+    // register set again) and dropped by the compiler -- its wait must not count on them
+    auto step = [&](int c, float (&cur)[8], float (&nxt)[8], int bufc, int bufn, bool tail)
+        __attribute__((always_inline)) {
         load_b(c + 2, nxt);   // unconditional (past C reads zeros): no branch for the waits to merge over
         if constexpr (DMA) issue_w(min(c + 2, nkc - 1), bufn);   // past the last chunk a harmless repeat
         __builtin_amdgcn_sched_barrier(0);   // issued here, ahead of this chunk's work
@@ -244,7 +247,10 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
             // wave's reads of chunk c are done (the next step's DMA overwrites it); a bare s_barrier:
             // __syncthreads()'s release fence would wait for every load in flight (vmcnt(0))
             __builtin_amdgcn_sched_barrier(0);
-            wait_vm<12>();
+            if (tail)
+                wait_vm<4>();   // (stricter than needed if the loads were kept: still correct)
+            else
+                wait_vm<12>();
             __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
@@ -258,12 +264,12 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
     int c = 0;
 #pragma unroll 1
     for (; c + 3 <= nkc; c += 3) {
-        step(c, bv[0], bv[2], 0, 2);
-        step(c + 1, bv[1], bv[0], 1, 0);
-        step(c + 2, bv[2], bv[1], 2, 1);
+        step(c, bv[0], bv[2], 0, 2, false);
+        step(c + 1, bv[1], bv[0], 1, 0, false);
+        step(c + 2, bv[2], bv[1], 2, 1, false);
     }
-    if (c < nkc) step(c, bv[0], bv[2], 0, 2);
-    if (c + 1 < nkc) step(c + 1, bv[1], bv[0], 1, 0);
+    if (c < nkc) step(c, bv[0], bv[2], 0, 2, true);
+    if (c + 1 < nkc) step(c + 1, bv[1], bv[0], 1, 0, true);
 
     // ---- epilogue: lane holds query q, channels 32 rb + 8 (r >> 2) + 4 kh + (r & 3)
     const __amdgpu_buffer_rsrc_t osrc = __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)b * O * Q, 0, O * Q * 4,

@@ -4,7 +4,7 @@ default mode) on arbitrary NCHW inputs, against an fp64 conv of the same fp32 in
 Bar (north star: the conv is floating point, normwise): max|got - ref| / rms(ref) <= 1e-5 over
 the outputs, for inputs whose per-query scales span 2^-40..2^40, all-zero query columns, weight
 rows at different scales, ragged Q (not a multiple of the 64-query tile) and O (not a multiple of
-the 256-channel tile), C = 81 / 243 / 324, with and without bias.  NaN in a query's column makes
+the 256-channel tile), C = 20 / 81 / 243 / 270 / 324 (every K-loop remainder), with and without bias.  NaN in a query's column makes
 exactly that query's outputs NaN (as the reference's conv: NaN * w propagates, relu(NaN) = NaN).
 """
 import numpy as np
@@ -50,8 +50,10 @@ def _normwise(got, ref):
     return float(np.max(np.abs(got.cpu().numpy().astype(np.float64) - ref)) / np.sqrt(np.mean(ref * ref)))
 
 
+# C = 324 / 81: 21 / 6 chunks (whole loop trips); 243: 16 (one remainder step); 270: 17 and 20: 2
+# (two remainder steps, the second after the first's DMA wait: the case the tail waits guard)
 @pytest.mark.parametrize("shape", [(2, 324, 4800, 256), (1, 324, 100, 256), (3, 243, 130, 96),
-                                   (1, 81, 64, 300), (2, 324, 1, 256)],
+                                   (1, 81, 64, 300), (2, 324, 1, 256), (1, 270, 300, 256), (2, 20, 200, 64)],
                          ids=lambda s: "b%d_c%d_q%d_o%d" % s)
 @pytest.mark.parametrize("with_bias", [True, False], ids=["bias", "nobias"])
 def test_dense_normwise(ea, shape, with_bias):

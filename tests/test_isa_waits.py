@@ -159,3 +159,61 @@ def test_checker_flags_a_hoisted_query_load(asm):
     early = ins[:bar] + [ins[p]] + [ln for i, ln in enumerate(ins[bar:], bar) if i != p]
     errs = check_loop(early, k["nbuf"], k["copies"], k["nk"], k["chunk"], True, k["span"])
     assert any("before barrier" in e for e in errs), errs
+
+
+# ---- conv.hip: conv1x1_split_kernel<true> (the split convc1) stages its weight chunks by LDS-DMA
+# through 3 buffers, two chunks ahead, and waits for chunk c + 1 at the end of step c with a static
+# vmcnt(12) (step c's 8 query-column loads + 4 DMA pieces are the only newer VMEM ops; vmcnt(4) in
+# the remainder steps, whose dead query-column loads the compiler drops -- this replay caught that
+# race when the remainder still waited vmcnt(12)).  Its K loop is
+# rolled (3 steps per trip) with a 0-2 step remainder, so the straight-line stream replayed here is
+# prologue + two trips of the loop body + both remainder steps: barriers 0 (prologue) .. 8.
+CONV = "conv1x1_split_kernelILb1EE"
+
+
+@pytest.fixture(scope="module")
+def conv_asm():
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not installed")
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "conv.s")
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                        "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S",
+                        os.path.join(CSRC, "conv.hip"), "-o", out],
+                       check=True, capture_output=True)
+        return open(out).read()
+
+
+def conv_stream(s):
+    """Straight-line replay of the conv kernel: prologue, loop body twice, the remainder steps."""
+    m = re.search(r"^(_Z\S*" + re.escape(CONV) + r"\S*):", s, re.M)
+    assert m, f"{CONV} not in the listing"
+    end = s.find(".Lfunc_end", m.start())
+    lines = s[m.start():end].splitlines()
+    # the K loop: the loop header whose body holds the MFMAs
+    heads = [i for i, ln in enumerate(lines) if "Inner Loop Header" in ln]
+    head = next(h for h in heads if any("v_mfma" in ln for ln in lines[h:h + 200]))
+    label = lines[head].split(":")[0]
+    back = next(i for i in range(head, len(lines)) if re.search(r"s_cbranch\S*\s+" + re.escape(label) + r"$",
+                                                                 lines[i].strip()))
+    last_bar = max(i for i, ln in enumerate(lines) if ln.strip() == "s_barrier")
+
+    def ins(a, b):
+        return [ln.strip() for ln in lines[a:b]
+                if ln.startswith("\t") and not ln.strip().startswith((".", ";"))]
+    return ins(0, head) + ins(head, back + 1) * 2 + ins(back + 1, last_bar + 1)
+
+
+def test_conv_static_waits_match_issue_order(conv_asm):
+    ins = conv_stream(conv_asm)
+    assert sum(1 for ln in ins if ln == "s_barrier") == 9
+    assert sum(1 for ln in ins if is_dma(ln)) == 4 * 10   # chunks 0 .. 9, 4 pieces per wave each
+    errs = check_loop(ins, nbuf=3, copies=4, nk=9, chunk=16384, check_offsets=False, span=1)
+    assert not errs, "\n".join(errs)
+
+
+def test_conv_checker_flags_a_short_wait(conv_asm):
+    """vmcnt(12) -> vmcnt(16) at the step barriers would let chunk c + 1's pieces be in flight."""
+    ins = [ln.replace("vmcnt(12)", "vmcnt(16)") for ln in conv_stream(conv_asm)]
+    errs = check_loop(ins, nbuf=3, copies=4, nk=9, chunk=16384, check_offsets=False, span=1)
+    assert any("DMA may be in flight" in e for e in errs), errs
