@@ -248,7 +248,7 @@ def cpu_baseline(f1, f2, coords, iters):
 
 def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
     """lookup + convc1 + ReLU (CorrBlock.lookup_conv1x1_relu) in both modes --
-    "split" (the default: ecorr_lookup, then the split-f16 ecorr_conv1x1_relu_split) and "fused"
+    "split" (the default: ecorr_lookup_qmax, then the split-f16 ecorr_conv1x1_relu_split) and "fused"
     (ecorr_lookup_conv1x1_relu_packed, one fp32-MFMA kernel) -- against the unfused path they replace
     (our lookup, then torch's conv2d + relu on MIOpen), 12 iterations, HIP events on the launch
     stream; outside the headline timed region.  `conv_split` times the split conv kernel alone on
@@ -278,12 +278,20 @@ def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
         split = run(lambda c: blk.lookup_conv1x1_relu(c, wgt, bias, mode="split"))
         unfused = run(lambda c: torch.relu(F.conv2d(blk(c), wgt, bias)))
         lookup = run(lambda c: blk(c))
-        corr = blk(coords[0])
+        corr = torch.empty((B, 324, H, W), device=device)
+        qmax = torch.empty((B, 12, Q), device=device)
+        _lib.check(_lib.lib().ecorr_lookup_qmax(blk._pyramid.data_ptr(), coords[0].contiguous().data_ptr(), B, H, W,
+                                                Q, 4, 4, corr.data_ptr(), qmax.data_ptr(), _lib.stream_of(corr)),
+                   "lookup qmax")
         out = torch.empty((B, 256, H, W), device=device)
         pk = _lib.packed_conv1x1_weight(wgt, 256, 324, "split")
-        conv = run(lambda c: _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
-            corr.data_ptr(), B, 324, Q, pk.data_ptr(), bias.data_ptr(), 256, out.data_ptr(),
-            _lib.stream_of(corr)), "split conv"))
+
+        def conv_fn(qm):
+            return lambda c: _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
+                corr.data_ptr(), B, 324, Q, None if qm is None else qm.data_ptr(), 12, pk.data_ptr(), bias.data_ptr(),
+                256, out.data_ptr(), _lib.stream_of(corr)), "split conv")
+        conv = run(conv_fn(qmax))
+        conv_pre = run(conv_fn(None))
     flops = 2.0 * B * Q * 256 * 324
     conv_bytes = 4.0 * B * Q * (324 + 256)
     default = os.environ.get("ECORR_CONVC1", "split")
@@ -296,11 +304,12 @@ def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
                            "unit": "TFLOP/s", "frac": round(flops / (best * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
                            "note": "the conv's 2*O*C flop per query over the whole lookup + convc1 time, "
                                    "against the fp32 MFMA peak (the split mode runs them as 3 f16 MFMAs each)"},
-            "conv_split": {"ms": round(conv, 4), "bound": "hbm",
+            "conv_split": {"ms": round(conv, 4), "ms_own_prepass": round(conv_pre, 4), "bound": "hbm",
                            "achieved": round(conv_bytes / (conv * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
                            "unit": "GB/s", "frac": round(conv_bytes / (conv * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                            "bytes": f"{conv_bytes:.4g} B: corr in (324 x 4 B) + out (256 x 4 B) per query "
-                                    "(the kernel reads corr twice: max pre-pass + K loop)"},
+                                    "(+ 12 x 4 B of per-query maxima from ecorr_lookup_qmax; ms_own_prepass: "
+                                    "without them, the kernel's own max pass re-reads corr)"},
             "work_per_launch": f"{flops:.4g} flop (1x1 conv 324->256 over B*H*W queries)"}
 
 
@@ -491,8 +500,9 @@ def measure_e2e(B, iters, device, reps=5):
     download-only).  Median of `reps` forwards after a warm-up, outside the headline timed region,
     for (a) the reference's CorrBlock op sequence on the GPU (bmm, avg_pool2d, grid_sample:
     oracle/torch_ref.py, a reference leg), (b) eraft_amd.CorrBlock in the reference's call pattern,
-    (c) (b) + the fused lookup/convc1 and the HIP convex upsampling; with the CorrBlock share of
-    each forward (build + iters lookups of that CorrBlock -- for (c) the fused lookup + convc1 --
+    (c) (b) + the HIP lookup + convc1 + ReLU (CorrBlock.lookup_conv1x1_relu in its default mode,
+    `convc1_mode`; the key keeps its round-3 name) and the HIP convex upsampling; with the CorrBlock
+    share of each forward (build + iters lookups of that CorrBlock -- for (c) the lookup + convc1 --
     timed alone on the same fmaps)."""
     import statistics
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -562,6 +572,8 @@ def measure_e2e(B, iters, device, reps=5):
             corr_ms = timed(corr_only(cls or eraft_amd.CorrBlock, fused))
             res[name] = {"ms_per_forward": round(ms, 3), "pairs_per_s": round(B / (ms * 1e-3), 2),
                          "corrblock_ms": round(corr_ms, 3), "corrblock_share": round(corr_ms / ms, 4)}
+            if fused:
+                res[name]["convc1_mode"] = os.environ.get("ECORR_CONVC1", "split")
         del fm1, fm2
     res["speedup_vs_reference_corrblock"] = round(res["reference_corrblock_ops_on_gpu"]["ms_per_forward"] /
                                                   res["eraft_amd_corrblock"]["ms_per_forward"], 3)

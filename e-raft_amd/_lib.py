@@ -54,10 +54,12 @@ SYMBOLS = {
     "ecorr_conv1x1_pack": (_i, [_p, _i, _i, _p, _p]),
     "ecorr_lookup_conv1x1_relu_packed": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _i, _p, _p]),
     # (O, C, bytes*) / (weight[O][C], O, C, packed, stream) /
-    # (in[B][C][Q], B, C, Q, packed, bias, O, out, stream): split-f16 convc1 + ReLU (ABI 15)
+    # (in[B][C][Q], B, C, Q, qmax, G, packed, bias, O, out, stream): split-f16 convc1 + ReLU (ABI 15)
     "ecorr_conv1x1_split_size": (_i, [_i, _i, ctypes.POINTER(_i64)]),
     "ecorr_conv1x1_split_pack": (_i, [_p, _i, _i, _p, _p]),
-    "ecorr_conv1x1_relu_split": (_i, [_p, _i, _i, _i, _p, _p, _i, _p, _p]),
+    "ecorr_conv1x1_relu_split": (_i, [_p, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p]),
+    # as ecorr_lookup + qmax[B][3*levels][q_count] (before stream)
+    "ecorr_lookup_qmax": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "ecorr_bilinear_sampler": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _p]),
     "ecorr_coords_grid": (_i, [_i, _i, _i, _p, _p]),
     # (chunks, chunk, world, B, C, H, W, out, stream)

@@ -113,8 +113,9 @@ class CorrBlock:
         BasicMotionEncoder.convc1 + ReLU (update.py:67,74).
         weight: [O, C, 1, 1] (or [O, C]) fp32 with C = num_levels * (2r+1)^2; bias: [O] or None.
         Returns [B, O, H, W].  mode (default: env ECORR_CONVC1, else "split"):
-          "split"  ecorr_lookup into a temporary [B, C, H, W], then ecorr_conv1x1_relu_split (f16
-                   matrix cores, split operands: normwise within 1e-5 of the fp32 conv);
+          "split"  ecorr_lookup_qmax into a temporary [B, C, H, W] (+ per-query maxima), then
+                   ecorr_conv1x1_relu_split (f16 matrix cores, split operands: normwise within 1e-5
+                   of the fp32 conv);
           "fused"  ecorr_lookup_conv1x1_relu_packed: one kernel, the lookup tile never leaves the
                    CU, an exact c-ordered fp32 MFMA sum (radius 4, num_levels <= 4, O a multiple of 64)."""
         mode = mode or os.environ.get("ECORR_CONVC1", "split")
@@ -147,9 +148,14 @@ class CorrBlock:
             st = _lib.stream_of(coords)
             if mode == "split":
                 wt = _lib.packed_conv1x1_weight(weight, O, C, "split")   # hi/lo f16 fragments, once per weight
-                corr = self(coords)
+                G = 3 * self.num_levels
+                corr = torch.empty((B, C, H, W), dtype=torch.float32, device=self._device)
+                qmax = torch.empty((B, G, H * W), dtype=torch.float32, device=self._device)
+                _lib.check(_lib.lib().ecorr_lookup_qmax(
+                    self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, self.num_levels, self.radius,
+                    corr.data_ptr(), qmax.data_ptr(), st), "CorrBlock lookup (split convc1)")
                 _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
-                    corr.data_ptr(), B, C, H * W, wt.data_ptr(), bptr, O, out.data_ptr(), st),
+                    corr.data_ptr(), B, C, H * W, qmax.data_ptr(), G, wt.data_ptr(), bptr, O, out.data_ptr(), st),
                     "CorrBlock lookup+conv1x1+relu (split)")
             else:
                 wt = _lib.packed_conv1x1_weight(weight, O, C)   # MFMA fragment order, re-laid once per weight

@@ -209,6 +209,16 @@ ECORR_EXPORT int ecorr_lookup(const float* pyramid, const float* coords, int B, 
     return launch_lookup(P, B, (hipStream_t)stream);
 }
 
+ECORR_EXPORT int ecorr_lookup_qmax(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
+                                   int levels, int radius, float* out, float* qmax, void* stream) {
+    if (!qmax) return ECORR_EINVAL;
+    LookupParams P{};
+    const int st = lookup_params(pyramid, coords, B, H, W, q_count, levels, radius, out, &P);
+    if (st != ECORR_OK) return st;
+    P.qmax = qmax;
+    return launch_lookup(P, B, (hipStream_t)stream);
+}
+
 ECORR_EXPORT int ecorr_lookup_conv1x1_relu(const float* pyramid, const float* coords, int B, int H, int W,
                                            int q_count, int levels, int radius, const float* weight,
                                            const float* bias, int O, float* out, void* stream) {
@@ -251,10 +261,10 @@ ECORR_EXPORT int ecorr_conv1x1_split_pack(const float* weight, int O, int C, voi
     return launch_conv1x1_split_pack(weight, O, C, packed, (hipStream_t)stream);
 }
 
-ECORR_EXPORT int ecorr_conv1x1_relu_split(const float* in, int B, int C, int Q, const void* packed,
-                                          const float* bias, int O, float* out, void* stream) {
+ECORR_EXPORT int ecorr_conv1x1_relu_split(const float* in, int B, int C, int Q, const float* qmax, int G,
+                                          const void* packed, const float* bias, int O, float* out, void* stream) {
     if (!in || !packed || !out) return ECORR_EINVAL;
-    return launch_conv1x1_relu_split(in, B, C, Q, packed, bias, O, out, (hipStream_t)stream);
+    return launch_conv1x1_relu_split(in, B, C, Q, qmax, G, packed, bias, O, out, (hipStream_t)stream);
 }
 
 ECORR_EXPORT int ecorr_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,

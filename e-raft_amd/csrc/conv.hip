@@ -112,6 +112,7 @@ __device__ __forceinline__ void wait_vm() {
 // chunks ahead, with static vmcnt waits; else through registers, two buffers, one chunk ahead.
 template <bool DMA>
 __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restrict__ in, int C, int Q,
+                                                            const float* __restrict__ qmax, int G,
                                                             const char* __restrict__ packed,
                                                             const float* __restrict__ bias, int O,
                                                             float* __restrict__ out) {
@@ -155,8 +156,13 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
         sbias[tid] = (bias && o < O) ? bias[o] : 0.f;
     }
 
-    // ---- pre-pass: the query's largest |value| over C -> its exponent
+    // ---- the query's largest |value| over C -> its exponent: from the lookup's partial maxima
+    // (ecorr_lookup_qmax) or a pre-pass over the column
     float m = 0.f;
+    if (qmax) {
+        if (qok)
+            for (int g = oh; g < G; g += 2) m = fmaxf(m, qmax[((int64_t)b * G + g) * Q + q]);
+    } else
 #pragma unroll 1
     for (int c = oh; c < nkc; c += 8) {   // 4 chunks' loads in flight at once (clamped repeats past C)
         float v[4][8];
@@ -308,8 +314,9 @@ int launch_conv1x1_split_pack(const float* wt, int O, int C, void* packed, hipSt
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
 }
 
-int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const void* packed, const float* bias, int O,
-                              float* out, hipStream_t stream) {
+int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const float* qmax, int G, const void* packed,
+                              const float* bias, int O, float* out, hipStream_t stream) {
+    if (qmax && G <= 0) return ECORR_EINVAL;
     if (B <= 0 || C <= 0 || Q <= 0 || O <= 0 || B > 65535 || split_oblocks(O) > 65535) return ECORR_EINVAL;
     // 32-bit buffer offsets: a lane past Q reads from C*Q on, the prefetch reaches 3 chunks past C; the stores
     // likewise from O*Q up to the output block's last row
@@ -318,8 +325,8 @@ int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const void* 
         return ECORR_EINVAL;
     if ((const void*)in == (const void*)out) return ECORR_EINVAL;
     const dim3 grid((unsigned)((Q + SQ - 1) / SQ), (unsigned)split_oblocks(O), (unsigned)B);
-    hipLaunchKernelGGL(conv1x1_split_kernel<kConvDMA>, grid, dim3(SNT), 0, stream, in, C, Q, (const char*)packed, bias, O,
-                       out);
+    hipLaunchKernelGGL(conv1x1_split_kernel<kConvDMA>, grid, dim3(SNT), 0, stream, in, C, Q, qmax, G,
+                       (const char*)packed, bias, O, out);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
 }

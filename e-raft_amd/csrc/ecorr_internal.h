@@ -63,6 +63,8 @@ struct LookupParams {
     int lh[ECORR_MAX_LEVELS], lw[ECORR_MAX_LEVELS];
     int lntx[ECORR_MAX_LEVELS];      // tiles per tile row (0 = compact row-major)
     int lsz[ECORR_MAX_LEVELS];       // floats per query image
+    float* qmax;          // null, or [B][3 * levels][q_count]: per-query partial maxima of |out|
+                          // (ecorr_lookup_qmax: the split convc1's column exponents)
 };
 
 int launch_lookup(const LookupParams& P, int B, hipStream_t stream);
@@ -74,8 +76,8 @@ int launch_conv1x1_pack(const float* wt, int O, int C, float* packed, hipStream_
 // conv.hip: split-f16 1x1 conv + ReLU on an NCHW tensor (ecorr_conv1x1_relu_split)
 int64_t conv1x1_split_bytes(int O, int C);
 int launch_conv1x1_split_pack(const float* wt, int O, int C, void* packed, hipStream_t stream);
-int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const void* packed, const float* bias, int O,
-                              float* out, hipStream_t stream);
+int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const float* qmax, int G, const void* packed,
+                              const float* bias, int O, float* out, hipStream_t stream);
 
 int launch_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,
                             int Hg, int Wg, float* out, float* mask, hipStream_t stream);

@@ -55,7 +55,9 @@ __global__ __launch_bounds__(4 * QB) void lookup_staged(LookupParams P) {
 // windows and their origins (31.7 KB at r = 4: 5 blocks per CU).  Round-1 A/B: the 4-thread
 // kernel with per-output k decoding 61 vs 48.5 us; chains shared through LDS 2.8% slower.
 // PAIR (every level width even): windows staged as 8-byte column pairs (lookup_stage.h).
-template <int R, int QB, bool PAIR>
+// QMAX: also the query's largest |sample| over this wave's columns of the level (fmaxf: NaN
+// ignored) -> P.qmax[b][3 lv + part][p], the split convc1's column exponent without a re-read.
+template <int R, int QB, bool PAIR, bool QMAX = false>
 __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
     constexpr int NTQ = 3 * QB, K = 2 * R + 1, AP = K / 3;
     static_assert(K % 3 == 0 && QB == kWave, "one wave per part, whole columns per part");
@@ -113,6 +115,7 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
         P.out + (int64_t)b * P.C * P.q_count, 0, P.C * P.q_count * 4, 0x00020000);
     const int voff = p * 4;
     const int sbase = lv * KK * P.q_count * 4;
+    float vmax = 0.0f;
     if (md == 0) {
         int yo[K];
 #pragma unroll
@@ -126,6 +129,7 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
             for (int bb = 0; bb < K; ++bb) {
                 const float* c = wc + yo[bb];
                 const float v = blend(c[0], c[1], c[SW], c[SW + 1], wx[ai], wy[bb]);
+                if constexpr (QMAX) vmax = fmaxf(vmax, fabsf(v));
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
                                                       sbase + (a * K + bb) * P.q_count * 4, 2);
             }
@@ -136,10 +140,24 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
 #pragma unroll
             for (int bb = 0; bb < K; ++bb) {
                 const float v = sample_direct(P, lv, b, p, fx[ai], fy[bb], wx[ai], wy[bb]);
+                if constexpr (QMAX) vmax = fmaxf(vmax, fabsf(v));
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
                                                       sbase + ((part * AP + ai) * K + bb) * P.q_count * 4, 2);
             }
     }
+    if constexpr (QMAX)
+        if (valid) P.qmax[((int64_t)b * 3 * P.levels + 3 * lv + part) * P.q_count + p] = vmax;
+}
+
+// Partial maxima for the lookups without a QMAX instantiation: thread = (b, query), the max of |out|
+// over all C channels into group 0, zeros into the other 3 * levels - 1.
+__global__ __launch_bounds__(NT) void qmax_kernel(LookupParams P, int B) {
+    const int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x;
+    if (i >= (int64_t)B * P.q_count) return;
+    const int64_t b = i / P.q_count, p = i % P.q_count, Q = P.q_count, G = 3 * P.levels;
+    float m = 0.0f;
+    for (int c = 0; c < P.C; ++c) m = fmaxf(m, fabsf(P.out[(b * P.C + c) * Q + p]));
+    for (int g = 0; g < G; ++g) P.qmax[(b * G + g) * Q + p] = g == 0 ? m : 0.0f;
 }
 
 // Any radius: one thread per output element, direct gather (reference-shaped; used for radii
@@ -204,16 +222,28 @@ inline int hip_status() {
 }  // namespace
 
 int launch_lookup(const LookupParams& P, int B, hipStream_t stream) {
+    // the paths without a QMAX instantiation: the lookup, then qmax_kernel over its output
+    auto done = [&]() {
+        const int st = hip_status();
+        if (st != ECORR_OK || !P.qmax) return st;
+        hipLaunchKernelGGL(qmax_kernel, dim3(grid_for((int64_t)B * P.q_count)), dim3(NT), 0, stream, P, B);
+        return hip_status();
+    };
     if (P.radius > 4) {
         const int64_t n = (int64_t)B * P.C * P.q_count;
         hipLaunchKernelGGL(lookup_direct, dim3(grid_for(n)), dim3(NT), 0, stream, P, B);
-        return hip_status();
+        return done();
     }
     const dim3 grid((unsigned)((P.q_count + 63) / 64), (unsigned)P.levels, (unsigned)B);
     const bool cols = (P.radius == 4 || P.radius == 1) && (int64_t)P.C * P.q_count * 4 < 0x7fffffff;
     if (cols) {
         bool pair = true;   // column-pair staging: every level width even, 8-byte aligned levels
         for (int lv = 0; lv < P.levels; ++lv) pair &= P.lw[lv] % 2 == 0 && (uintptr_t)P.lvl[lv] % 8 == 0;
+        if (P.radius == 4 && P.qmax) {
+            if (pair) hipLaunchKernelGGL((lookup_cols_reg<4, 64, true, true>), grid, dim3(192), 0, stream, P);
+            else hipLaunchKernelGGL((lookup_cols_reg<4, 64, false, true>), grid, dim3(192), 0, stream, P);
+            return hip_status();
+        }
         if (P.radius == 4) {
             if (pair) hipLaunchKernelGGL((lookup_cols_reg<4, 64, true>), grid, dim3(192), 0, stream, P);
             else hipLaunchKernelGGL((lookup_cols_reg<4, 64, false>), grid, dim3(192), 0, stream, P);
@@ -221,7 +251,7 @@ int launch_lookup(const LookupParams& P, int B, hipStream_t stream) {
             if (pair) hipLaunchKernelGGL((lookup_cols_reg<1, 64, true>), grid, dim3(192), 0, stream, P);
             else hipLaunchKernelGGL((lookup_cols_reg<1, 64, false>), grid, dim3(192), 0, stream, P);
         }
-        return hip_status();
+        return done();
     }
     switch (P.radius) {
         case 0: hipLaunchKernelGGL((lookup_staged<0, 64>), grid, dim3(256), 0, stream, P); break;
@@ -230,7 +260,7 @@ int launch_lookup(const LookupParams& P, int B, hipStream_t stream) {
         case 3: hipLaunchKernelGGL((lookup_staged<3, 64>), grid, dim3(256), 0, stream, P); break;
         default: hipLaunchKernelGGL((lookup_staged<4, 64>), grid, dim3(256), 0, stream, P); break;
     }
-    return hip_status();
+    return done();
 }
 
 int launch_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,

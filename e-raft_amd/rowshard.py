@@ -273,11 +273,17 @@ class RowShardedCorrBlock:
         with _lib.on_device(self._device):
             if mode == "split":
                 wt = _lib.packed_conv1x1_weight(weight, O, C, "split")
+                G = 3 * self.num_levels
                 corr = torch.empty((B, C, self.q_count), dtype=torch.float32, device=self._device)
-                self._lookup_into(coords_rows, corr)
+                qmax = torch.empty((B, G, self.q_count), dtype=torch.float32, device=self._device)
+                _lib.check(_lib.lib().ecorr_lookup_qmax(
+                    self._pyramid.data_ptr(), coords_rows.data_ptr(), B, H, W, self.q_count, self.num_levels,
+                    self.radius, corr.data_ptr(), qmax.data_ptr(), _lib.stream_of(out)),
+                    "RowShardedCorrBlock lookup (split convc1)")
                 _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
-                    corr.data_ptr(), B, C, self.q_count, wt.data_ptr(), None if bias is None else bias.data_ptr(),
-                    O, out.data_ptr(), _lib.stream_of(out)), "RowShardedCorrBlock lookup+conv1x1+relu (split)")
+                    corr.data_ptr(), B, C, self.q_count, qmax.data_ptr(), G, wt.data_ptr(),
+                    None if bias is None else bias.data_ptr(), O, out.data_ptr(), _lib.stream_of(out)),
+                    "RowShardedCorrBlock lookup+conv1x1+relu (split)")
                 return out if self.world == 1 else self._ex.gather(B, O, W, self._device)
             wt = _lib.packed_conv1x1_weight(weight, O, C)   # MFMA fragment order, re-laid once per weight
             _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu_packed(

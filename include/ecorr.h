@@ -106,6 +106,12 @@ int ecorr_build_split_gemm(int B, int D, int H, int W, int q_count, int levels, 
 int ecorr_lookup(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
                  int levels, int radius, float* out, void* stream);
 
+/* ecorr_lookup + per-query partial maxima for ecorr_conv1x1_relu_split (ABI 15): qmax
+ * float[B][3*levels][q_count], max over its 3*levels entries of query p = max_c |out[b][c][p]|
+ * (fmaxf: NaN ignored); out bitwise what ecorr_lookup writes.  Replaces: corr.py:29-50 as above. */
+int ecorr_lookup_qmax(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
+                      int levels, int radius, float* out, float* qmax, void* stream);
+
 /* Lookup fused with its consumer, BasicMotionEncoder's convc1 + ReLU:
  * out float[B][O][q_count] = relu(bias[o] + sum_c weight[o][c] * corr[b][c][p]), where corr is
  * exactly what ecorr_lookup would return (C = levels*(2r+1)^2 channels) and never leaves the chip.
@@ -138,12 +144,15 @@ int ecorr_lookup_conv1x1_relu_packed(const float* pyramid, const float* coords, 
  * ecorr_conv1x1_split_size gives the packed weight's byte count, ecorr_conv1x1_split_pack writes it
  * from weight float[O][C] (stream-ordered); valid until the weight changes.  bias float[O] or NULL;
  * in and out must not overlap (ECORR_EINVAL when they are the same pointer, or when the 32-bit
- * buffer offsets, about (2C + 64) * Q * 4 bytes, would overflow).
+ * buffer offsets, about (2C + 64) * Q * 4 bytes, would overflow).  qmax: NULL (the kernel finds each
+ * query's largest |in| itself, one extra pass over in) or float[B][G][Q] partial maxima whose max
+ * over g is max_c |in[b][c][p]| (fmaxf semantics, NaN ignored) -- what ecorr_lookup_qmax writes
+ * with G = 3 * levels; the result is bitwise the same either way.
  * Replaces: F.relu(self.convc1(corr)) (update.py:67,74). */
 int ecorr_conv1x1_split_size(int O, int C, int64_t* bytes);
 int ecorr_conv1x1_split_pack(const float* weight, int O, int C, void* packed, void* stream);
-int ecorr_conv1x1_relu_split(const float* in, int B, int C, int Q, const void* packed, const float* bias, int O,
-                             float* out, void* stream);
+int ecorr_conv1x1_relu_split(const float* in, int B, int C, int Q, const float* qmax, int G, const void* packed,
+                             const float* bias, int O, float* out, void* stream);
 
 /* Generic bilinear_sampler: img float[N][C][h][w], coords float[N][Hg][Wg][2] in pixels ->
  * out float[N][C][Hg][Wg]; mask (nullable) float[N][Hg][Wg] = 1 where the normalized sample

@@ -127,12 +127,16 @@ def test_argument_validation_before_launch(ea):
     assert L.ecorr_conv1x1_split_size(0, 324, ctypes.byref(n)) == _lib.ECORR_EINVAL
     assert L.ecorr_conv1x1_split_pack(None, 256, 324, 8, None) == _lib.ECORR_EINVAL
     assert L.ecorr_conv1x1_split_pack(8, 256, 0, 8, None) == _lib.ECORR_EINVAL
-    S = L.ecorr_conv1x1_relu_split   # (in, B, C, Q, packed, bias, O, out, stream)
-    assert S(None, 1, 324, 4800, 8, None, 256, 16, None) == _lib.ECORR_EINVAL
-    assert S(8, 1, 324, 4800, None, None, 256, 16, None) == _lib.ECORR_EINVAL
-    assert S(8, 0, 324, 4800, 8, None, 256, 16, None) == _lib.ECORR_EINVAL
-    assert S(8, 1, 324, 4800, 8, None, 256, 8, None) == _lib.ECORR_EINVAL   # in == out
-    assert S(8, 1, 324, 1 << 20, 8, None, 256, 16, None) == _lib.ECORR_EINVAL   # 32-bit offsets
+    S = L.ecorr_conv1x1_relu_split   # (in, B, C, Q, qmax, G, packed, bias, O, out, stream)
+    assert S(None, 1, 324, 4800, None, 0, 8, None, 256, 16, None) == _lib.ECORR_EINVAL
+    assert S(8, 1, 324, 4800, None, 0, None, None, 256, 16, None) == _lib.ECORR_EINVAL
+    assert S(8, 0, 324, 4800, None, 0, 8, None, 256, 16, None) == _lib.ECORR_EINVAL
+    assert S(8, 1, 324, 4800, None, 0, 8, None, 256, 8, None) == _lib.ECORR_EINVAL   # in == out
+    assert S(8, 1, 324, 1 << 20, None, 0, 8, None, 256, 16, None) == _lib.ECORR_EINVAL   # 32-bit offsets
+    assert S(8, 1, 324, 4800, 24, 0, 8, None, 256, 16, None) == _lib.ECORR_EINVAL   # qmax without G
+    # lookup + partial maxima: a qmax buffer is required, then validates like ecorr_lookup
+    assert L.ecorr_lookup_qmax(8, 8, 1, 8, 8, 64, 4, 4, 8, None, None) == _lib.ECORR_EINVAL
+    assert L.ecorr_lookup_qmax(8, 8, 1, 8, 8, 64, 4, 33, 8, 8, None) == _lib.ECORR_ERADIUS
     # the split build's stages validate like the whole call (no workspace / no operands)
     assert L.ecorr_build_split_pack(8, 8, 1, 256, 8, 8, 64, None, None) == _lib.ECORR_EINVAL
     assert L.ecorr_build_split_pack(None, 8, 1, 256, 8, 8, 64, 256, None) == _lib.ECORR_EINVAL

@@ -33,7 +33,7 @@ def _conv_split(x, w, bias):
     pk = _lib.packed_conv1x1_weight(w, O, C, "split")
     out = torch.empty((B, O, Q), dtype=torch.float32, device=DEV)
     _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
-        x.data_ptr(), B, C, Q, pk.data_ptr(), None if bias is None else bias.data_ptr(), O, out.data_ptr(),
+        x.data_ptr(), B, C, Q, None, 0, pk.data_ptr(), None if bias is None else bias.data_ptr(), O, out.data_ptr(),
         _lib.stream_of(x)), "split conv")
     torch.cuda.synchronize()
     return out
@@ -125,5 +125,44 @@ def test_in_out_alias_rejected(ea):
     x = torch.zeros((1, 324, 64), device=DEV)
     w = torch.zeros((256, 324), device=DEV)
     pk = _lib.packed_conv1x1_weight(w, 256, 324, "split")
-    assert _lib.lib().ecorr_conv1x1_relu_split(x.data_ptr(), 1, 324, 64, pk.data_ptr(), None, 256, x.data_ptr(),
-                                               _lib.stream_of(x)) == _lib.ECORR_EINVAL
+    assert _lib.lib().ecorr_conv1x1_relu_split(x.data_ptr(), 1, 324, 64, None, 0, pk.data_ptr(), None, 256,
+                                               x.data_ptr(), _lib.stream_of(x)) == _lib.ECORR_EINVAL
+    y = torch.zeros((1, 256, 64), device=DEV)
+    assert _lib.lib().ecorr_conv1x1_relu_split(x.data_ptr(), 1, 324, 64, x.data_ptr(), 0, pk.data_ptr(), None, 256,
+                                               y.data_ptr(), _lib.stream_of(x)) == _lib.ECORR_EINVAL   # G <= 0
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 16, 24, 4, 4), (1, 32, 23, 40, 3, 4), (1, 32, 16, 16, 4, 3),
+                                   (1, 16, 12, 12, 2, 5)], ids=lambda s: "b%d_d%d_%dx%d_l%d_r%d" % s)
+def test_lookup_qmax_and_conv_with_it(ea, shape):
+    """ecorr_lookup_qmax: out bitwise ecorr_lookup's, the max over each query's 3*levels partial maxima
+    = max_c |out| (radius 4: in the lookup kernel; other radii: the generic pass); the conv fed these
+    maxima is bitwise the conv that finds them itself (same exponents)."""
+    from eraft_amd import _lib
+    B, D, H, W, L, R = shape
+    C, O, Q, G = L * (2 * R + 1) ** 2, 256, H * W, 3 * L
+    f1 = torch.from_numpy(prng.normal(241, (B, D, H, W))).to(DEV)
+    f2 = torch.from_numpy(prng.normal(242, (B, D, H, W))).to(DEV)
+    coords = torch.from_numpy(prng.coords_with_flow(243, B, H, W, 3.0)).to(DEV)
+    coords[0, :, 0, :2] = torch.tensor([float("nan"), 1e9], device=DEV)   # direct-gather queries
+    w = torch.from_numpy(prng.normal(244, (O, C)) * np.float32(0.05)).to(DEV)
+    with torch.no_grad():
+        blk = ea.CorrBlock(f1, f2, num_levels=L, radius=R)
+        ref = blk(coords)
+        out = torch.empty_like(ref)
+        qmax = torch.full((B, G, Q), float("nan"), device=DEV)
+        _lib.check(_lib.lib().ecorr_lookup_qmax(blk._pyramid.data_ptr(), coords.data_ptr(), B, H, W, Q, L, R,
+                                                out.data_ptr(), qmax.data_ptr(), _lib.stream_of(coords)), "qmax")
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+        want = ref.view(B, C, Q).abs().nan_to_num(nan=0.0).amax(dim=1)
+        assert torch.equal(qmax.amax(dim=1), want)
+        pk = _lib.packed_conv1x1_weight(w, O, C, "split")
+        a = torch.empty((B, O, Q), device=DEV)
+        b = torch.empty((B, O, Q), device=DEV)
+        for dst, qm in ((a, None), (b, qmax)):
+            _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
+                out.data_ptr(), B, C, Q, None if qm is None else qm.data_ptr(), G, pk.data_ptr(), None, O,
+                dst.data_ptr(), _lib.stream_of(out)), "conv")
+        torch.cuda.synchronize()
+        assert torch.equal(a.nan_to_num(nan=7.0), b.nan_to_num(nan=7.0))

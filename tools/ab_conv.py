@@ -3,7 +3,8 @@
 tree's libecorr.so and AB_ALT_LIB lab builds (name=path,...) in one process, at DSEC B=16 60x80 on
 a materialized lookup (C = 324 -> O = 256).  Reports each library's normwise error (max|d| / rms)
 against an fp64 conv, whether its output is bitwise the tree's, and the median time of 20 calls per
-round over rotated rounds.  AB_CONV_IID=1: an i.i.d. normal input instead of a real lookup."""
+round over rotated rounds.  AB_CONV_IID=1: an i.i.d. normal input instead of a real lookup;
+AB_CONV_PRE=1: no per-query maxima passed (the kernel's own max pre-pass)."""
 import ctypes
 import json
 import os
@@ -52,9 +53,19 @@ for name, L in LIBS.items():
     packed[name] = pk
 
 
+# per-query partial maxima as ecorr_lookup_qmax leaves them (G = 12 groups; here one group holds the
+# max, the rest 0) unless AB_CONV_PRE=1 (the kernel's own pre-pass)
+G = 12
+qmax = None
+if not os.environ.get("AB_CONV_PRE"):
+    qmax = torch.zeros((B, G, Q), device="cuda")
+    qmax[:, 0] = x.abs().nan_to_num(nan=0.0).amax(dim=1)
+
+
 def run(name):
-    _lib.check(LIBS[name].ecorr_conv1x1_relu_split(x.data_ptr(), B, C, Q, packed[name].data_ptr(), bias.data_ptr(),
-                                                   O, out.data_ptr(), st), "conv")
+    _lib.check(LIBS[name].ecorr_conv1x1_relu_split(x.data_ptr(), B, C, Q, None if qmax is None else qmax.data_ptr(), G,
+                                                   packed[name].data_ptr(), bias.data_ptr(), O, out.data_ptr(), st),
+               "conv")
 
 
 with torch.no_grad():
