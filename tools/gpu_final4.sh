@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-3 final: every GPU test, smoke, the headline bench + C3 / C5 lines, a 2-rank batch-sharded
+# Round-4 final: every GPU test, smoke, the headline bench + C3 / C5 lines, a 2-rank batch-sharded
 # rehearsal on one GPU (gloo), then the rocprof kernel trace and the PMC passes (C2 full set, C3 /
-# C5 traffic).  usage: tools/gpu_final3.sh TAG
-cd "$GRAFT_REPO_ROOT"; TAG=${1:-r3final}; OUT=gpurun_out/$TAG; mkdir -p $OUT
+# C5 traffic).  usage: tools/gpu_final4.sh TAG
+cd "$GRAFT_REPO_ROOT"; TAG=${1:-r4final}; OUT=gpurun_out/$TAG; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E 'FAILED|ERROR|passed|failed' $OUT/pytest_gpu.log | tail -8; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
@@ -27,3 +27,8 @@ for f in sorted(glob.glob(sys.argv[1] + "/bench*.log")):
 PY
 [ -n "$NOPROF" ] && exit 0
 bash tools/profile.sh $TAG/prof
+rc=$?; [ $rc -ne 0 ] && exit $rc
+# the SURVEY §8f rows (split / fused convc1, upsampling, splat, voxel) under the kernel trace, no e2e
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof/kt_next -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $OUT/prof/kt_next.log 2>&1
+rc=$?; echo "kt next rc=$rc"; exit $rc
