@@ -1014,6 +1014,10 @@ PATCHES["mo_wsst"] = [
 
 # split convc1 (conv.hip): weight chunks through registers instead of LDS-DMA
 PATCHES["cv_regw"] = [("conv.hip", "constexpr bool kConvDMA = true;", "constexpr bool kConvDMA = false;")]
+# split convc1: non-temporal output stores
+PATCHES["cv_nt"] = [("conv.hip", """__builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), osrc, obase + (ob * SO + ol + t) * qs, 0,
+                                                      0);""", """__builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), osrc, obase + (ob * SO + ol + t) * qs, 0,
+                                                      2);""")]
 
 
 def build(name):
