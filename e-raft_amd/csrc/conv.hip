@@ -20,15 +20,15 @@
 //
 // Workgroup = 64 queries x 256 output channels, 4 waves: wave w owns query block qb = w & 1 (32
 // queries: the MFMA's N) and channel half oh = w >> 1 (4 x 32 channels: M), 4 accumulator tiles.
-//   pre-pass  per query the max |corr| over C (each wave half of the chunks, lanes = queries,
-//             combined through LDS) -> e_p;
+//   maxima    per query the max |corr| over C -> e_p: from the lookup's partial maxima
+//             (ecorr_lookup_qmax), else a pre-pass (each wave half of the chunks, combined in LDS);
 //   K loop    per 16-channel chunk: the weight chunk (16 KB, the A fragments of all 8 channel
 //             blocks, hi and lo, pre-split and laid out in fragment order by ecorr_conv1x1_split_pack)
-//             goes global -> registers -> LDS one chunk ahead, double-buffered, one barrier per chunk;
+//             goes global -> LDS by LDS-DMA two chunks ahead, three buffers, one barrier per chunk;
 //             the B fragment (lane = query, 8 consecutive channels) is loaded from corr as 8 dwords
-//             two chunks ahead, split in registers; 4 x 3 MFMAs per wave.
+//             PD chunks ahead, split in registers; 4 x 3 MFMAs per wave.
 // Work: 2*O*C flop per query (12.7 GFLOP at DSEC B=16) as 3 f16 MFMAs per product; bytes: corr in
-// (C*4 per query, read twice: the max pre-pass and the K loop) + out (O*4 per query).
+// (C*4 per query; twice without the partial maxima) + out (O*4 per query, non-temporal stores).
 
 #include "ecorr_device.h"
 #include "ecorr_internal.h"
@@ -108,15 +108,17 @@ __device__ __forceinline__ void wait_vm() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// DMA: the weight chunks go global -> LDS by LDS-DMA (no staging registers), three buffers, two
-// chunks ahead, with static vmcnt waits; else through registers, two buffers, one chunk ahead.
-template <bool DMA>
+// The weight chunks go global -> LDS by LDS-DMA (no staging registers; through registers it was
+// 63.9 vs 53.9 us, profiles/r04_lab/r4l_ab_conv.txt), three buffers, two chunks ahead, with static
+// vmcnt waits (tests/test_isa_waits.py replays them on the emitted ISA); the query columns are
+// loaded PD chunks ahead into PD + 1 fixed register sets.
+template <int PD>
 __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restrict__ in, int C, int Q,
                                                             const float* __restrict__ qmax, int G,
                                                             const char* __restrict__ packed,
                                                             const float* __restrict__ bias, int O,
                                                             float* __restrict__ out) {
-    constexpr int NB = DMA ? 3 : 2;
+    constexpr int NB = 3;
     // ALL LDS in one object: with a second __shared__ object hipcc waits vmcnt(0) before every
     // ds_read while an LDS-DMA is in flight (cdna_hip_programming.md, the second-__shared__ trap)
     struct Lds {
@@ -176,19 +178,8 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
     m = fmaxf(m, __shfl_xor(m, 32));
     if (kh == 0) red[oh][qi] = m;
 
-    uintx4 wr[4];
-    auto load_w = [&](int c) __attribute__((always_inline)) {
-        const uintx4* p = reinterpret_cast<const uintx4*>(wsrc + (int64_t)c * SCHUNK);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) wr[i] = p[tid + SNT * i];
-    };
-    auto store_w = [&](int buf) __attribute__((always_inline)) {
-        uintx4* p = reinterpret_cast<uintx4*>(wbuf[buf]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) p[tid + SNT * i] = wr[i];
-    };
-    // DMA: wave w copies the chunk's 1-KB pieces w, w + 4, w + 8, w + 12 (lane-linear, as LDS-DMA
-    // writes them), the chunk offset in the scalar soffset
+    // wave w copies the chunk's 1-KB pieces w, w + 4, w + 8, w + 12 (lane-linear, as LDS-DMA writes
+    // them), the chunk offset in the scalar soffset
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wsrc), 0, nkc * SCHUNK, 0x00020000);
     auto issue_w = [&](int c, int buf) __attribute__((always_inline)) {
@@ -198,25 +189,16 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
                 wrs, (__attribute__((address_space(3))) void*)(wbuf[buf] + (w + 4 * s) * 1024), 16,
                 (w + 4 * s) * 1024 + lane * 16, c * SCHUNK, 0, 0);
     };
-    float bv[3][8];   // B values of chunks c, c + 1, c + 2 (three fixed register sets: no copies)
-    if constexpr (DMA) {
-        issue_w(0, 0);
-        issue_w(nkc > 1 ? 1 : 0, 1);
-        load_b(0, bv[0]);
-        load_b(1, bv[1]);   // past C: out of range, zeros
-        __builtin_amdgcn_sched_barrier(0);
-        wait_vm<20>();      // chunk 0's pieces (then chunk 1's 4 and 2 x 8 B loads may be in flight)
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): red / sex / sbias written
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    } else {
-        load_w(0);
-        store_w(0);
-        load_w(nkc > 1 ? 1 : 0);
-        load_b(0, bv[0]);
-        load_b(1, bv[1]);   // past C: out of range, zeros
-        __syncthreads();
-    }
+    float bv[PD + 1][8];   // B values of chunks c .. c + PD (fixed register sets: no copies)
+    issue_w(0, 0);
+    issue_w(nkc > 1 ? 1 : 0, 1);
+#pragma unroll
+    for (int k = 0; k < PD; ++k) load_b(k, bv[k]);   // past C: out of range, zeros
+    __builtin_amdgcn_sched_barrier(0);
+    wait_vm<4 + 8 * PD>();   // chunk 0's pieces (chunk 1's 4 and PD x 8 B loads may be in flight)
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): red / sex / sbias written
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
     const int eq = split_exponent(fmaxf(red[0][qi], red[1][qi]));
     const float sq = pow2(eq);
 
@@ -226,19 +208,18 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
 
-    // ---- K loop: chunk c's weights in wbuf[c & 1] (published by the barrier before); its B values
-    // in set cur, and chunk c + 2's loads go to set nxt (chunk c - 1's, consumed)
-    // (DMA: chunk c in wbuf[c % 3], bufc; chunk c + 2 goes to bufn = (c + 2) % 3, chunk c - 1's)
+    // ---- K loop, step c: chunk c's weights in wbuf[c % 3] (published by the barrier before),
+    // chunk c + 2's DMA into wbuf[(c + 2) % 3] (chunk c - 1's, whose readers passed that barrier);
+    // chunk c's B values in set cur, chunk c + PD's loads into set nxt (chunk c - 1's, consumed).
     // tail: a remainder step after the loop, whose query-column loads are dead (nothing reads that
     // register set again) and dropped by the compiler -- its wait must not count on them
-    auto step = [&](int c, float (&cur)[8], float (&nxt)[8], int bufc, int bufn, bool tail)
-        __attribute__((always_inline)) {
-        load_b(c + 2, nxt);   // unconditional (past C reads zeros): no branch for the waits to merge over
-        if constexpr (DMA) issue_w(min(c + 2, nkc - 1), bufn);   // past the last chunk a harmless repeat
+    auto step = [&](int c, float (&cur)[8], float (&nxt)[8], bool tail) __attribute__((always_inline)) {
+        load_b(c + PD, nxt);   // unconditional (past C reads zeros): no branch for the waits to merge over
+        issue_w(min(c + 2, nkc - 1), (c + 2) % NB);   // past the last chunk a harmless repeat
         __builtin_amdgcn_sched_barrier(0);   // issued here, ahead of this chunk's work
         halfx8 bh, bl;
         split8(cur, sq, bh, bl);
-        const char* wb = wbuf[DMA ? bufc : (c & 1)] + lane * 16;
+        const char* wb = wbuf[c % NB] + lane * 16;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int rb = 4 * oh + i;
@@ -248,34 +229,27 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
             acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[i], 0, 0, 0);
             acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[i], 0, 0, 0);
         }
-        if constexpr (DMA) {
-            // chunk c + 1's pieces landed (only this step's 8 B loads + 4 pieces may be newer) and this
-            // wave's reads of chunk c are done (the next step's DMA overwrites it); a bare s_barrier:
-            // __syncthreads()'s release fence would wait for every load in flight (vmcnt(0))
-            __builtin_amdgcn_sched_barrier(0);
-            if (tail)
-                wait_vm<4>();   // (stricter than needed if the loads were kept: still correct)
-            else
-                wait_vm<12>();
-            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-        } else {
-            store_w((c + 1) & 1);   // its readers (chunk c - 1) passed the last barrier; past the
-            load_w(min(c + 2, nkc - 1));   // last chunk a harmless repeat
-            __builtin_amdgcn_sched_barrier(0);
-            __syncthreads();
-        }
+        // chunk c + 1's pieces landed (only this step's 8 B loads + 4 pieces may be newer) and this
+        // wave's reads of chunk c are done (the next step's DMA overwrites it); a bare s_barrier:
+        // __syncthreads()'s release fence would wait for every load in flight (vmcnt(0))
+        __builtin_amdgcn_sched_barrier(0);
+        if (tail)
+            wait_vm<4>();   // (stricter than needed if the loads were kept: still correct)
+        else
+            wait_vm<12>();
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
     };
     int c = 0;
 #pragma unroll 1
-    for (; c + 3 <= nkc; c += 3) {
-        step(c, bv[0], bv[2], 0, 2, false);
-        step(c + 1, bv[1], bv[0], 1, 0, false);
-        step(c + 2, bv[2], bv[1], 2, 1, false);
+    for (; c + PD + 1 <= nkc; c += PD + 1) {
+#pragma unroll
+        for (int k = 0; k <= PD; ++k) step(c + k, bv[k], bv[(k + PD) % (PD + 1)], false);
     }
-    if (c < nkc) step(c, bv[0], bv[2], 0, 2, true);
-    if (c + 1 < nkc) step(c + 1, bv[1], bv[0], 1, 0, true);
+#pragma unroll
+    for (int k = 0; k < PD; ++k)
+        if (c + k < nkc) step(c + k, bv[k], bv[(k + PD) % (PD + 1)], true);
 
     // ---- epilogue: lane holds query q, channels 32 rb + 8 (r >> 2) + 4 kh + (r & 3)
     const __amdgpu_buffer_rsrc_t osrc = __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)b * O * Q, 0, O * Q * 4,
@@ -294,12 +268,12 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
                 v = v + bo[t];   // a missing bias is 0 (v + 0 = v for every v but -0, which ReLU maps to 0)
                 v = v < 0.f ? 0.f : v;   // torch.relu: NaN stays NaN
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), osrc, obase + (ob * SO + ol + t) * qs, 0,
-                                                      0);
+                                                      2);   // nt: 52.2 vs 53.9 us (r4l_ab_conv.txt)
             }
         }
 }
 
-constexpr bool kConvDMA = true;
+constexpr int kConvPD = 2;   // query-column prefetch distance (chunks)
 
 }  // namespace
 
@@ -325,7 +299,7 @@ int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const float*
         return ECORR_EINVAL;
     if ((const void*)in == (const void*)out) return ECORR_EINVAL;
     const dim3 grid((unsigned)((Q + SQ - 1) / SQ), (unsigned)split_oblocks(O), (unsigned)B);
-    hipLaunchKernelGGL(conv1x1_split_kernel<kConvDMA>, grid, dim3(SNT), 0, stream, in, C, Q, qmax, G,
+    hipLaunchKernelGGL(conv1x1_split_kernel<kConvPD>, grid, dim3(SNT), 0, stream, in, C, Q, qmax, G,
                        (const char*)packed, bias, O, out);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;

@@ -161,14 +161,14 @@ def test_checker_flags_a_hoisted_query_load(asm):
     assert any("before barrier" in e for e in errs), errs
 
 
-# ---- conv.hip: conv1x1_split_kernel<true> (the split convc1) stages its weight chunks by LDS-DMA
+# ---- conv.hip: conv1x1_split_kernel<2> (the split convc1, query columns 2 chunks ahead) stages its weight chunks by LDS-DMA
 # through 3 buffers, two chunks ahead, and waits for chunk c + 1 at the end of step c with a static
 # vmcnt(12) (step c's 8 query-column loads + 4 DMA pieces are the only newer VMEM ops; vmcnt(4) in
 # the remainder steps, whose dead query-column loads the compiler drops -- this replay caught that
 # race when the remainder still waited vmcnt(12)).  Its K loop is
 # rolled (3 steps per trip) with a 0-2 step remainder, so the straight-line stream replayed here is
 # prologue + two trips of the loop body + both remainder steps: barriers 0 (prologue) .. 8.
-CONV = "conv1x1_split_kernelILb1EE"
+CONV = "conv1x1_split_kernelILi2EE"
 
 
 @pytest.fixture(scope="module")

@@ -1012,12 +1012,9 @@ PATCHES["mo_wsst"] = [
 ]
 
 
-# split convc1 (conv.hip): weight chunks through registers instead of LDS-DMA
-PATCHES["cv_regw"] = [("conv.hip", "constexpr bool kConvDMA = true;", "constexpr bool kConvDMA = false;")]
-# split convc1: non-temporal output stores
-PATCHES["cv_nt"] = [("conv.hip", """__builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), osrc, obase + (ob * SO + ol + t) * qs, 0,
-                                                      0);""", """__builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), osrc, obase + (ob * SO + ol + t) * qs, 0,
-                                                      2);""")]
+# split convc1 (conv.hip): query columns 3 / 4 chunks ahead instead of 2
+PATCHES["cv_pf3"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 3;")]
+PATCHES["cv_pf4"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 4;")]
 
 
 def build(name):
