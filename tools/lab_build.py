@@ -1013,6 +1013,16 @@ PATCHES["mo_wsst"] = [
 
 
 # split convc1 (conv.hip): query columns 3 / 4 chunks ahead instead of 2
+# the QMAX lookup (split convc1 path) with default-policy output stores instead of nt (corr stays in
+# the caches for the conv that reads it next)
+PATCHES["lk_qplain"] = [("lookup.hip", """                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
+                                                      sbase + (a * K + bb) * P.q_count * 4, 2);""",
+                         """                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
+                                                      sbase + (a * K + bb) * P.q_count * 4, QMAX ? 0 : 2);""")]
+# split convc1: non-temporal query-column loads (read once)
+PATCHES["cv_bnt"] = [("conv.hip", "v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, off + j * qs, 0, 0));",
+                      "v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, off + j * qs, 0, 2));")]
+COMBOS["qplain_bnt"] = ["lk_qplain", "cv_bnt"]
 PATCHES["cv_pf3"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 3;")]
 PATCHES["cv_pf4"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 4;")]
 
