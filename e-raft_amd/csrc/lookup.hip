@@ -115,6 +115,10 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
         P.out + (int64_t)b * P.C * P.q_count, 0, P.C * P.q_count * 4, 0x00020000);
     const int voff = p * 4;
     const int sbase = lv * KK * P.q_count * 4;
+    // output stores: non-temporal (round 3: 42.4 vs 46.9 us plain); the QMAX lookup's corr is read
+    // right back by the split convc1, so it keeps the default policy and the corr stays in the
+    // caches: lookup + conv 97.4 vs 111.0 us (profiles/r04_lab/r4o_ab_qmax.txt)
+    constexpr int kOutAux = QMAX ? 0 : 2;
     float vmax = 0.0f;
     if (md == 0) {
         int yo[K];
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
                 const float v = blend(c[0], c[1], c[SW], c[SW + 1], wx[ai], wy[bb]);
                 if constexpr (QMAX) vmax = fmaxf(vmax, fabsf(v));
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
-                                                      sbase + (a * K + bb) * P.q_count * 4, 2);
+                                                      sbase + (a * K + bb) * P.q_count * 4, kOutAux);
             }
         }
     } else {   // coordinates that do not fit the window: exact direct gather
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
                 const float v = sample_direct(P, lv, b, p, fx[ai], fy[bb], wx[ai], wy[bb]);
                 if constexpr (QMAX) vmax = fmaxf(vmax, fabsf(v));
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
-                                                      sbase + ((part * AP + ai) * K + bb) * P.q_count * 4, 2);
+                                                      sbase + ((part * AP + ai) * K + bb) * P.q_count * 4, kOutAux);
             }
     }
     if constexpr (QMAX)
