@@ -152,18 +152,53 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
             v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, off + j * qs, 0, 0));
     };
 
-    {
-        const int o = ob * SO + tid;
-        sex[tid] = reinterpret_cast<const int*>(packed + (int64_t)nob * nkc * SCHUNK)[o];
-        sbias[tid] = (bias && o < O) ? bias[o] : 0.f;
-    }
+    // wave w copies the chunk's 1-KB pieces w, w + 4, w + 8, w + 12 (lane-linear, as LDS-DMA writes
+    // them), the chunk offset in the scalar soffset
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wsrc), 0, nkc * SCHUNK, 0x00020000);
+    auto issue_w = [&](int c, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                wrs, (__attribute__((address_space(3))) void*)(wbuf[buf] + (w + 4 * s) * 1024), 16,
+                (w + 4 * s) * 1024 + lane * 16, c * SCHUNK, 0, 0);
+    };
+
+    // ---- prologue: every load in flight before the first wait (one memory latency, not five):
+    // chunks 0-1's weights, chunks 0 .. PD-1's query columns, this block's row exponents and biases,
+    // the query's partial maxima
+    float bv[PD + 1][8];   // B values of chunks c .. c + PD (fixed register sets: no copies)
+    issue_w(0, 0);
+    issue_w(nkc > 1 ? 1 : 0, 1);
+#pragma unroll
+    for (int k = 0; k < PD; ++k) load_b(k, bv[k]);   // past C: out of range, zeros
+    // (bias and maxima through range-checked buffers: a null pointer is a 0-byte range reading 0 --
+    // no branches, whose merged wait states cost a full drain here)
+    const int eo_t = reinterpret_cast<const int*>(packed + (int64_t)nob * nkc * SCHUNK)[ob * SO + tid];
+    const __amdgpu_buffer_rsrc_t brs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bias), 0, bias ? O * 4 : 0, 0x00020000);
+    const float bo_t = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (ob * SO + tid) * 4, 0, 0));
+    constexpr int QG = 6;   // partial maxima per wave and pass (G = 12 for 4 levels: one pass)
+    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(qmax ? qmax + (int64_t)b * G * Q : nullptr), 0, qmax ? G * Q * 4 : 0, 0x00020000);
+    const int qc = min(q, Q - 1);
+    float qv[QG];
+#pragma unroll
+    for (int i = 0; i < QG; ++i)
+        qv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(qrs, (min(oh + 2 * i, G - 1) * Q + qc) * 4, 0, 0));
+    __builtin_amdgcn_sched_barrier(0);
+    sex[tid] = eo_t;
+    sbias[tid] = bo_t;
 
     // ---- the query's largest |value| over C -> its exponent: from the lookup's partial maxima
-    // (ecorr_lookup_qmax) or a pre-pass over the column
+    // (ecorr_lookup_qmax; clamped repeats are harmless) or a pre-pass over the column
     float m = 0.f;
     if (qmax) {
-        if (qok)
-            for (int g = oh; g < G; g += 2) m = fmaxf(m, qmax[((int64_t)b * G + g) * Q + q]);
+#pragma unroll
+        for (int i = 0; i < QG; ++i) m = fmaxf(m, qv[i]);
+        for (int g = oh + 2 * QG; g < G; g += 2)
+            m = fmaxf(m, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(qrs, (g * Q + qc) * 4, 0, 0)));
+        m = qok ? m : 0.f;
     } else
 #pragma unroll 1
     for (int c = oh; c < nkc; c += 8) {   // 4 chunks' loads in flight at once (clamped repeats past C)
@@ -177,23 +212,6 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
     }
     m = fmaxf(m, __shfl_xor(m, 32));
     if (kh == 0) red[oh][qi] = m;
-
-    // wave w copies the chunk's 1-KB pieces w, w + 4, w + 8, w + 12 (lane-linear, as LDS-DMA writes
-    // them), the chunk offset in the scalar soffset
-    const __amdgpu_buffer_rsrc_t wrs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wsrc), 0, nkc * SCHUNK, 0x00020000);
-    auto issue_w = [&](int c, int buf) __attribute__((always_inline)) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                wrs, (__attribute__((address_space(3))) void*)(wbuf[buf] + (w + 4 * s) * 1024), 16,
-                (w + 4 * s) * 1024 + lane * 16, c * SCHUNK, 0, 0);
-    };
-    float bv[PD + 1][8];   // B values of chunks c .. c + PD (fixed register sets: no copies)
-    issue_w(0, 0);
-    issue_w(nkc > 1 ? 1 : 0, 1);
-#pragma unroll
-    for (int k = 0; k < PD; ++k) load_b(k, bv[k]);   // past C: out of range, zeros
     __builtin_amdgcn_sched_barrier(0);
     wait_vm<4 + 8 * PD>();   // chunk 0's pieces (chunk 1's 4 and PD x 8 B loads may be in flight)
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): red / sex / sbias written
@@ -290,7 +308,7 @@ int launch_conv1x1_split_pack(const float* wt, int O, int C, void* packed, hipSt
 
 int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const float* qmax, int G, const void* packed,
                               const float* bias, int O, float* out, hipStream_t stream) {
-    if (qmax && G <= 0) return ECORR_EINVAL;
+    if (qmax && (G <= 0 || (int64_t)G * Q * 4 >= 0x7fffffffLL)) return ECORR_EINVAL;
     if (B <= 0 || C <= 0 || Q <= 0 || O <= 0 || B > 65535 || split_oblocks(O) > 65535) return ECORR_EINVAL;
     // 32-bit buffer offsets: a lane past Q reads from C*Q on, the prefetch reaches 3 chunks past C; the stores
     // likewise from O*Q up to the output block's last row
