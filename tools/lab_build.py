@@ -1023,6 +1023,9 @@ PATCHES["lk_qplain"] = [("lookup.hip", """                __builtin_amdgcn_raw_b
 PATCHES["cv_bnt"] = [("conv.hip", "v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, off + j * qs, 0, 0));",
                       "v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, off + j * qs, 0, 2));")]
 COMBOS["qplain_bnt"] = ["lk_qplain", "cv_bnt"]
+# the QMAX lookup's output stores with sc1 (16) / nt | sc1 (18) instead of the default policy
+PATCHES["lk_qsc1"] = [("lookup.hip", "constexpr int kOutAux = QMAX ? 0 : 2;", "constexpr int kOutAux = QMAX ? 16 : 2;")]
+PATCHES["lk_qntsc1"] = [("lookup.hip", "constexpr int kOutAux = QMAX ? 0 : 2;", "constexpr int kOutAux = QMAX ? 18 : 2;")]
 PATCHES["cv_pf3"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 3;")]
 PATCHES["cv_pf4"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 4;")]
 
