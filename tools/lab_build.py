@@ -1026,6 +1026,26 @@ COMBOS["qplain_bnt"] = ["lk_qplain", "cv_bnt"]
 # the QMAX lookup's output stores with sc1 (16) / nt | sc1 (18) instead of the default policy
 PATCHES["lk_qsc1"] = [("lookup.hip", "constexpr int kOutAux = QMAX ? 0 : 2;", "constexpr int kOutAux = QMAX ? 16 : 2;")]
 PATCHES["lk_qntsc1"] = [("lookup.hip", "constexpr int kOutAux = QMAX ? 0 : 2;", "constexpr int kOutAux = QMAX ? 18 : 2;")]
+# lookup_cols_reg dispatch order: all level-0 workgroups first (the longest: the largest image),
+# then levels 1..3 fill the last round (LPT for the drain tail) -- or the reverse
+_LK_OLD = """    const int lv = blockIdx.y, b = blockIdx.z;
+    const int q0 = blockIdx.x * QB;
+    const int p = q0 + g;"""
+def _lk_lvmajor(rev):
+    return [("lookup.hip", _LK_OLD, """    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int per = gridDim.x * gridDim.z;
+    const int lvo = lin / per, rr = lin - lvo * per;
+    const int lv = %s, b = rr / gridDim.x;
+    const int q0 = (rr - b * gridDim.x) * QB;
+    const int p = q0 + g;""" % ("gridDim.y - 1 - lvo" if rev else "lvo"))]
+# ... or the level fastest: a query group's four level workgroups dispatched back to back
+PATCHES["lk_lvminor"] = [("lookup.hip", _LK_OLD, """    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int lv = lin % gridDim.y, xb = lin / gridDim.y;
+    const int b = xb / gridDim.x;
+    const int q0 = (xb - b * gridDim.x) * QB;
+    const int p = q0 + g;""")]
+PATCHES["lk_lvmajor"] = _lk_lvmajor(False)
+PATCHES["lk_lvmajor_rev"] = _lk_lvmajor(True)
 PATCHES["cv_pf3"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 3;")]
 PATCHES["cv_pf4"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 4;")]
 
