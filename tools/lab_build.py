@@ -1049,6 +1049,53 @@ PATCHES["lk_lvmajor_rev"] = _lk_lvmajor(True)
 PATCHES["cv_pf3"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 3;")]
 PATCHES["cv_pf4"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 4;")]
 
+# ---- round 5: is the lookup concurrency-bound?  LDS padded so that 4 / 3 workgroups fit a CU
+# instead of 5 (timing only, bitwise the same); and de-phased first rounds (a share of the first
+# 1280 workgroups sleeps ~3.8 / ~1.9 us before its coordinate loads)
+def _lk_pad(nf):
+    return [("lookup.hip", """    __shared__ WB st;
+    const int tid = threadIdx.x, g = tid % QB;
+    const int part = __builtin_amdgcn_readfirstlane(tid / QB);   // wave-uniform""", """    __shared__ WB st;
+    __shared__ float lk_pad[%d];
+    const int tid = threadIdx.x, g = tid %% QB;
+    if (P.q_count == -12345) { lk_pad[tid] = 1.0f; __syncthreads(); P.out[tid] = lk_pad[(tid + 1) %% 192]; }
+    const int part = __builtin_amdgcn_readfirstlane(tid / QB);   // wave-uniform""" % nf)]
+PATCHES["lk_occ4"] = _lk_pad(2048)
+PATCHES["lk_occ3"] = _lk_pad(5000)
+def _lk_sleep(n, mod):
+    return [("lookup.hip", """    __shared__ WB st;
+    const int tid = threadIdx.x, g = tid % QB;
+    const int part = __builtin_amdgcn_readfirstlane(tid / QB);   // wave-uniform""", """    __shared__ WB st;
+    {
+        const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        if (lin < 1280 && (lin >> 8) %% %d == 1) __builtin_amdgcn_s_sleep(%d);
+    }
+    const int tid = threadIdx.x, g = tid %% QB;
+    const int part = __builtin_amdgcn_readfirstlane(tid / QB);   // wave-uniform""" % (mod, n))]
+PATCHES["lk_sleep127"] = _lk_sleep(127, 2)
+PATCHES["lk_sleep64"] = _lk_sleep(64, 2)
+
+# ---- round 5: where the lookup's time goes -- the same instructions with the window loads and / or
+# the output stores out of range (no memory traffic; timing only)
+PATCHES["lk_ldoob"] = [("lookup_stage.h", "__builtin_amdgcn_raw_buffer_load_b64(rsrc, need ? off : OOB, 0, 0);",
+                        "__builtin_amdgcn_raw_buffer_load_b64(rsrc, need ? OOB : OOB + (off & 4), 0, 0);")]
+PATCHES["lk_stoob"] = [("lookup.hip", "P.out + (int64_t)b * P.C * P.q_count, 0, P.C * P.q_count * 4, 0x00020000);",
+                        "P.out + (int64_t)b * P.C * P.q_count, 0, P.q_count == -1 ? 4 : 0, 0x00020000);")]
+COMBOS["lk_bothoob"] = ["lk_ldoob", "lk_stoob"]
+
+# the same on lookup_win (round 5)
+PATCHES["lkw_ldoob"] = [("lookup.hip", "(rsrc, (need ? off : OOB) + ry * WK::STEP, 0, 0);", "(rsrc, OOB + ry * WK::STEP + (need ? 0 : 4), 0, 0);")]
+COMBOS["lkw_bothoob"] = ["lkw_ldoob", "lk_stoob"]
+
+# lookup_win output store policy (aux bits: 1 sc0, 2 nt, 16 sc1) and window-load policy
+for _a in (1, 3, 16, 17, 19):
+    PATCHES[f"lkw_st{_a}"] = [("lookup.hip", "constexpr int kOutAux = QMAX ? 0 : 2;\n    auto store", f"constexpr int kOutAux = QMAX ? 0 : {_a};\n    auto store")]
+for _a in (1, 16, 17):
+    PATCHES[f"lkw_ld{_a}"] = [("lookup.hip", "(rsrc, (need ? off : OOB) + ry * WK::STEP, 0, 0);", f"(rsrc, (need ? off : OOB) + ry * WK::STEP, 0, {_a});")]
+
+# recipe-name prefix -> the lab_patches diff it applies on top of
+PREDIFF = {"qs": "build_qs.diff", "lkw_": "lookup_win.diff"}
+
 
 def build(name):
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
@@ -1057,6 +1104,9 @@ def build(name):
     shutil.copytree(os.path.join(ROOT, "e-raft_amd", "csrc"), os.path.join(dst, "e-raft_amd", "csrc"),
                     ignore=shutil.ignore_patterns("build"))
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(dst, "include"))
+    # recipes on top of a rejected variant kept as a diff (tools/lab_patches/): apply it first
+    for diff in sorted({d for n in COMBOS.get(name, [name]) for pre, d in PREDIFF.items() if n.startswith(pre)}):
+        subprocess.run(["patch", "-s", "-p1", "-d", dst, "-i", os.path.join(ROOT, "tools", "lab_patches", diff)], check=True)
     for fname, old, new in [x for n in COMBOS.get(name, [name]) for x in PATCHES[n]]:
         p = os.path.join(dst, "e-raft_amd", "csrc", fname)
         s = open(p).read()
