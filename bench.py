@@ -284,7 +284,7 @@ def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
                                                 Q, 4, 4, corr.data_ptr(), qmax.data_ptr(), _lib.stream_of(corr)),
                    "lookup qmax")
         out = torch.empty((B, 256, H, W), device=device)
-        pk = _lib.packed_conv1x1_weight(wgt, 256, 324, "split")
+        pk = _lib.packed_conv1x1_weight(wgt, 256, 324, "split", _lib.stream_of(wgt), {})
 
         def conv_fn(qm):
             return lambda c: _lib.check(_lib.lib().ecorr_conv1x1_relu_split(

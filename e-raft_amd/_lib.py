@@ -219,40 +219,32 @@ def build_pyramid(fmap1, fmap2, B, D, H, W, q_count, levels, off, what, mode=Non
     return pyr
 
 
-# Packed convc1 weights per weight tensor: (id, kind) -> (weakref, version, O, C, packed).  kind
-# "fused": ecorr_conv1x1_pack (the fused lookup + convc1 kernel's fp32 MFMA fragment order); "split":
-# ecorr_conv1x1_split_pack (hi/lo f16 fragments + row exponents for ecorr_conv1x1_relu_split).
-# ERAFT.forward calls convc1 `iters` times per forward with the same weight, so the weight is
-# re-laid once and again only after an in-place update (the tensor's version counter) -- or on
-# every call for tensors without a version counter (inference-mode tensors).
-_packed_weights = {}
-
-
-def packed_conv1x1_weight(weight, O, C, kind="fused"):
-    import weakref
+# Packed convc1 weights.  kind "fused": ecorr_conv1x1_pack (the fused lookup + convc1 kernel's fp32
+# MFMA fragment order); "split": ecorr_conv1x1_split_pack (hi/lo f16 fragments + row exponents for
+# ecorr_conv1x1_relu_split).  ERAFT.forward builds one CorrBlock per forward and calls convc1 `iters`
+# times with the same weight, so the caller passes a cache it owns (the CorrBlock instance's): the
+# weight is re-laid once per block.  The key holds the tensor identity, its storage pointer and its
+# version counter; a change through .data that keeps all three (w.data.mul_(...)) between two calls
+# of ONE block is not seen -- weights are fixed during a forward.  The pack runs on the consumer's
+# stream `st`, so the lookups that read it are ordered after it.
+def packed_conv1x1_weight(weight, O, C, kind, st, cache):
     try:
         version = weight._version
-    except RuntimeError:   # inference tensor: no version counter, no caching
-        version = None
-    key = (id(weight), kind)
-    ent = _packed_weights.get(key)
-    if (version is not None and ent is not None and ent[0]() is weight and ent[1] == version
-            and ent[2:4] == (O, C) and ent[4].device == weight.device):
-        return ent[4]
+    except RuntimeError:   # inference tensor: no version counter
+        version = -1
+    key = (kind, O, C)
+    ent = cache.get(key)
+    if ent is not None and ent[0] is weight and ent[1] == (weight.data_ptr(), version):
+        return ent[2]
     wt = weight.reshape(O, C).contiguous()
     n = ctypes.c_int64()
     if kind == "split":
         check(lib().ecorr_conv1x1_split_size(O, C, ctypes.byref(n)), "convc1 split weight pack")
         packed = torch.empty(n.value, dtype=torch.uint8, device=weight.device)
-        check(lib().ecorr_conv1x1_split_pack(wt.data_ptr(), O, C, packed.data_ptr(), stream_of(weight)),
-              "convc1 split weight pack")
+        check(lib().ecorr_conv1x1_split_pack(wt.data_ptr(), O, C, packed.data_ptr(), st), "convc1 split weight pack")
     else:
         check(lib().ecorr_conv1x1_packed_size(O, C, ctypes.byref(n)), "convc1 weight pack")
         packed = torch.empty(n.value, dtype=torch.float32, device=weight.device)
-        check(lib().ecorr_conv1x1_pack(wt.data_ptr(), O, C, packed.data_ptr(), stream_of(weight)),
-              "convc1 weight pack")
-    if version is not None:
-        for k in [k for k, e in _packed_weights.items() if e[0]() is None]:
-            del _packed_weights[k]
-        _packed_weights[key] = (weakref.ref(weight), version, O, C, packed)
+        check(lib().ecorr_conv1x1_pack(wt.data_ptr(), O, C, packed.data_ptr(), st), "convc1 weight pack")
+    cache[key] = (weight, (weight.data_ptr(), version), packed)
     return packed

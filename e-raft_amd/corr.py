@@ -78,6 +78,7 @@ class CorrBlock:
                                                "CorrBlock build")
         self._rows = B * Q
         self._levels_cache = None
+        self._wcache = {}   # packed convc1 weights of this block (_lib.packed_conv1x1_weight)
 
     @property
     def corr_pyramid(self):
@@ -147,7 +148,7 @@ class CorrBlock:
             out = torch.empty((B, O, H, W), dtype=torch.float32, device=self._device)
             st = _lib.stream_of(coords)
             if mode == "split":
-                wt = _lib.packed_conv1x1_weight(weight, O, C, "split")   # hi/lo f16 fragments, once per weight
+                wt = _lib.packed_conv1x1_weight(weight, O, C, "split", st, self._wcache)   # once per block
                 G = 3 * self.num_levels
                 corr = torch.empty((B, C, H, W), dtype=torch.float32, device=self._device)
                 qmax = torch.empty((B, G, H * W), dtype=torch.float32, device=self._device)
@@ -158,7 +159,7 @@ class CorrBlock:
                     corr.data_ptr(), B, C, H * W, qmax.data_ptr(), G, wt.data_ptr(), bptr, O, out.data_ptr(), st),
                     "CorrBlock lookup+conv1x1+relu (split)")
             else:
-                wt = _lib.packed_conv1x1_weight(weight, O, C)   # MFMA fragment order, re-laid once per weight
+                wt = _lib.packed_conv1x1_weight(weight, O, C, "fused", st, self._wcache)   # once per block
                 _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu_packed(
                     self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, self.num_levels,
                     self.radius, wt.data_ptr(), bptr, O, out.data_ptr(), st), "CorrBlock lookup+conv1x1+relu")

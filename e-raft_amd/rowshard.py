@@ -173,6 +173,7 @@ class RowShardedCorrBlock:
 
     def _init_local(self, fmap1_rows, fmap2, num_levels, radius):
         self.num_levels, self.radius = num_levels, radius
+        self._wcache = {}   # packed convc1 weights of this block (_lib.packed_conv1x1_weight)
         B, D, H, W = fmap2.shape
         self._shape = (B, D, H, W)
         self._device = fmap2.device
@@ -272,7 +273,7 @@ class RowShardedCorrBlock:
             out = self._ex.send_slab(B, O, W, device=self._device)
         with _lib.on_device(self._device):
             if mode == "split":
-                wt = _lib.packed_conv1x1_weight(weight, O, C, "split")
+                wt = _lib.packed_conv1x1_weight(weight, O, C, "split", _lib.stream_of(out), self._wcache)
                 G = 3 * self.num_levels
                 corr = torch.empty((B, C, self.q_count), dtype=torch.float32, device=self._device)
                 qmax = torch.empty((B, G, self.q_count), dtype=torch.float32, device=self._device)
@@ -285,7 +286,7 @@ class RowShardedCorrBlock:
                     None if bias is None else bias.data_ptr(), O, out.data_ptr(), _lib.stream_of(out)),
                     "RowShardedCorrBlock lookup+conv1x1+relu (split)")
                 return out if self.world == 1 else self._ex.gather(B, O, W, self._device)
-            wt = _lib.packed_conv1x1_weight(weight, O, C)   # MFMA fragment order, re-laid once per weight
+            wt = _lib.packed_conv1x1_weight(weight, O, C, "fused", _lib.stream_of(out), self._wcache)
             _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu_packed(
                 self._pyramid.data_ptr(), coords_rows.data_ptr(), B, H, W, self.q_count, self.num_levels,
                 self.radius, wt.data_ptr(), None if bias is None else bias.data_ptr(), O, out.data_ptr(),

@@ -30,7 +30,7 @@ def _conv_split(x, w, bias):
     from eraft_amd import _lib
     B, C, Q = x.shape
     O = w.shape[0]
-    pk = _lib.packed_conv1x1_weight(w, O, C, "split")
+    pk = _lib.packed_conv1x1_weight(w, O, C, "split", _lib.stream_of(w), {})
     out = torch.empty((B, O, Q), dtype=torch.float32, device=DEV)
     _lib.check(_lib.lib().ecorr_conv1x1_relu_split(
         x.data_ptr(), B, C, Q, None, 0, pk.data_ptr(), None if bias is None else bias.data_ptr(), O, out.data_ptr(),
@@ -107,8 +107,85 @@ def test_nan_column_propagates(ea):
     assert _normwise(torch.from_numpy(got[:, :, keep]), ref[:, :, keep]) <= 1e-5
 
 
+def test_block_weight_cache_data_mutation(ea):
+    """CorrBlock.lookup_conv1x1_relu(mode="split") packs the weight once per block: a change through
+    .data (no version bump) is seen by the next block, a new storage (.data = t) by the
+    same block; each result equals the split conv of the lookup with the weight as it is now."""
+    B, D, H, W = 2, 64, 16, 24
+    with torch.no_grad():
+        f1 = torch.from_numpy(prng.normal(241, (B, D, H, W))).to(DEV)
+        f2 = torch.from_numpy(prng.normal(242, (B, D, H, W))).to(DEV)
+        coords = torch.from_numpy(prng.coords_with_flow(243, B, H, W, 3.0)).to(DEV)
+        w = torch.from_numpy(prng.normal(244, (256, 324, 1, 1)) * np.float32(0.05)).to(DEV)
+
+        def want(blk):
+            return _conv_split(blk(coords).view(B, 324, H * W), w.view(256, 324), None).view(B, 256, H, W)
+
+        blk = ea.CorrBlock(f1, f2)
+        a = blk.lookup_conv1x1_relu(coords, w, None, mode="split")
+        assert torch.equal(a, want(blk))
+        w.data.mul_(-1.0)
+        blk2 = ea.CorrBlock(f1, f2)
+        b = blk2.lookup_conv1x1_relu(coords, w, None, mode="split")
+        assert torch.equal(b, want(blk2)) and not torch.equal(a, b)
+        w.data = w.data * 2.0
+        c = blk2.lookup_conv1x1_relu(coords, w, None, mode="split")
+        assert torch.equal(c, want(blk2)) and not torch.equal(b, c)
+
+
+@pytest.mark.parametrize("levels", [4, 2])
+def test_split_conv_nonfinite_golden(ea, levels):
+    """the split convc1 on the non-finite golden's fmaps (tests/golden/nonfinite_corr.npz)
+    built in fp32 mode, whose lookup holds +-inf and NaN samples as the reference's does.  The
+    documented deviation (conv.hip header): every output of a query holding a non-finite
+    sample is NaN (the split's lo half of an inf is inf - inf) where the reference's fp32 conv + ReLU
+    gives +-inf / 0 / NaN; every other output finite and normwise within 1e-5 of the reference conv
+    (update.py:74).  The fused mode keeps the reference's pattern (its fp32 sum: +inf where only +inf
+    terms meet, NaN where +inf and -inf do, 0 after ReLU for -inf).  At 4 levels every query's level-3
+    window holds a non-finite pooled column; at 2 levels some queries stay finite."""
+    import os
+    from conftest import GOLDEN
+    from test_oracle_golden import _load, _nonfinite_fmaps
+    z = _load(os.path.join(GOLDEN, "nonfinite_corr.npz"))
+    f1n, f2n = _nonfinite_fmaps(z)
+    r = int(z["r"])
+    C = levels * (2 * r + 1) ** 2
+    O = 64
+    f1, f2 = torch.from_numpy(f1n).to(DEV), torch.from_numpy(f2n).to(DEV)
+    coords = torch.from_numpy(z["coords_s3"]).to(DEV)
+    w = torch.from_numpy(prng.normal(251, (O, C)) * np.float32(0.05)).to(DEV)
+    bias = torch.from_numpy(prng.normal(252, (O,)) * np.float32(0.1)).to(DEV)
+    prev = ea._lib.build_mode()
+    ea._lib.set_build_mode("fp32")
+    try:
+        with torch.no_grad():
+            blk = ea.CorrBlock(f1, f2, num_levels=levels, radius=r)
+            corr = blk(coords)
+            split = blk.lookup_conv1x1_relu(coords, w, bias, mode="split")
+            fused = blk.lookup_conv1x1_relu(coords, w, bias, mode="fused")
+    finally:
+        ea._lib.set_build_mode(prev)
+    corr64 = corr.double().cpu()
+    ref = torch.relu(torch.einsum("oc,bchw->bohw", w.double().cpu(), corr64) + bias.double().cpu()[None, :, None, None])
+    bad = ~torch.isfinite(corr64).all(dim=1)   # [B, H, W]: queries with a non-finite sample
+    assert bad.any()
+    split = split.cpu().permute(0, 2, 3, 1)
+    assert torch.isnan(split[bad]).all()
+    good = ~bad
+    if levels == 2:
+        assert good.any()
+    if good.any():
+        assert torch.isfinite(split[good]).all()
+        got_g = split[good].double()
+        ref_g = ref.permute(0, 2, 3, 1)[good]
+        assert float((got_g - ref_g).abs().max() / ref_g.pow(2).mean().sqrt()) <= 1e-5
+    # the fused fp32 kernel: the reference's non-finite pattern
+    fused = fused.cpu().double()
+    assert torch.equal(torch.isnan(fused), torch.isnan(ref)) and torch.equal(torch.isinf(fused), torch.isinf(ref))
+
+
 def test_weight_repack_on_update(ea):
-    """The packed split weight is cached per weight tensor and re-made after an in-place update."""
+    """An in-place update of the weight between two packs gives the updated conv."""
     B, C, Q, O = 1, 324, 256, 256
     x = torch.from_numpy(prng.normal(231, (B, C, Q))).to(DEV)
     w = torch.from_numpy(prng.normal(232, (O, C)) * np.float32(0.05)).to(DEV)
@@ -124,7 +201,7 @@ def test_in_out_alias_rejected(ea):
     from eraft_amd import _lib
     x = torch.zeros((1, 324, 64), device=DEV)
     w = torch.zeros((256, 324), device=DEV)
-    pk = _lib.packed_conv1x1_weight(w, 256, 324, "split")
+    pk = _lib.packed_conv1x1_weight(w, 256, 324, "split", _lib.stream_of(w), {})
     assert _lib.lib().ecorr_conv1x1_relu_split(x.data_ptr(), 1, 324, 64, None, 0, pk.data_ptr(), None, 256,
                                                x.data_ptr(), _lib.stream_of(x)) == _lib.ECORR_EINVAL
     y = torch.zeros((1, 256, 64), device=DEV)
@@ -157,7 +234,7 @@ def test_lookup_qmax_and_conv_with_it(ea, shape):
         assert torch.equal(out.view(torch.int32), ref.view(torch.int32))   # bitwise (NaN samples too)
         want = ref.view(B, C, Q).abs().nan_to_num(nan=0.0).amax(dim=1)
         assert torch.equal(qmax.amax(dim=1), want)
-        pk = _lib.packed_conv1x1_weight(w, O, C, "split")
+        pk = _lib.packed_conv1x1_weight(w, O, C, "split", _lib.stream_of(w), {})
         a = torch.empty((B, O, Q), device=DEV)
         b = torch.empty((B, O, Q), device=DEV)
         for dst, qm in ((a, None), (b, qmax)):

@@ -128,3 +128,21 @@ def test_packed_weight_matches_weight_as_stored(ea, shape):
             ref.data_ptr(), _lib.stream_of(coords)), "unpacked")
         torch.cuda.synchronize()
         assert torch.equal(got2, ref) and not torch.equal(got2, got)
+        # changes through .data keep the version counter -- the packed weight is scoped
+        # to the block (one ERAFT forward), so the next block packs the weight as it is now ...
+        wgt.data.mul_(2.0)
+        blk2 = _block(ea, B, D, H, W, 51, L)
+        got3 = blk2.lookup_conv1x1_relu(coords, wgt, bias, mode="fused")
+        _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu(
+            blk2._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, L, 4, wgt.data_ptr(), bias.data_ptr(), O,
+            ref.data_ptr(), _lib.stream_of(coords)), "unpacked")
+        torch.cuda.synchronize()
+        assert torch.equal(got3, ref) and not torch.equal(got3, got2)
+        # ... and a new storage behind the same tensor (.data = t) re-packs within the block
+        wgt.data = wgt.data * -0.5
+        got4 = blk2.lookup_conv1x1_relu(coords, wgt, bias, mode="fused")
+        _lib.check(_lib.lib().ecorr_lookup_conv1x1_relu(
+            blk2._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, L, 4, wgt.data_ptr(), bias.data_ptr(), O,
+            ref.data_ptr(), _lib.stream_of(coords)), "unpacked")
+        torch.cuda.synchronize()
+        assert torch.equal(got4, ref) and not torch.equal(got4, got3)

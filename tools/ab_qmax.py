@@ -25,7 +25,7 @@ with torch.no_grad():
     qmax = torch.empty((B, 12, Q), device="cuda")
     wgt = torch.randn((256, 324), generator=g, device="cuda") * 0.05
     bias = torch.randn((256,), generator=g, device="cuda") * 0.1
-    pk = _lib.packed_conv1x1_weight(wgt, 256, 324, "split")
+    pk = _lib.packed_conv1x1_weight(wgt, 256, 324, "split", _lib.stream_of(wgt), {})
     res = torch.empty((B, 256, H, W), device="cuda")
 import ctypes  # noqa: E402
 LIBS = {"tree": _lib.lib()}
