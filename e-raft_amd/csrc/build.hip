@@ -835,9 +835,11 @@ __device__ __forceinline__ void split16_epilogue(const BuildParams& P, floatx4 (
     };
     // FULL: lane-constant offsets (query-row term qn of the 16-query group, the lane's piece; FOOB
     // where the piece lies outside the level) plus a wave-uniform term (qg, the store, the wave's
-    // 64-row group = its index: rl0 == 0) -- one v_add per store.  (The uniform term as the
-    // instruction's scalar soffset instead dropped ~0.03% of the level-0 stores at B = 16 on gfx950,
-    // round-3 tools/diag_full.py; added into the voffset every store lands.)
+    // 64-row group = its index: rl0 == 0) -- one v_add per store.  The uniform term stays in the
+    // voffset, soffset 0: with it in an SGPR soffset hipcc omits the wait state a 16-byte store needs
+    // before a VALU overwrites its data VGPRs (LLVM assumes that hazard only without an soffset
+    // register), and such a store wrote the next VALU's value (round 3's "lost" rows; round 5,
+    // tools/soff_repro.py; guarded by tests/test_isa_store_hazard.py).
     constexpr int FOOB = 0x70000000;   // + any uniform term stays beyond every slab, below 2^31
     const int qwu = __builtin_amdgcn_readfirstlane(qw);   // wave-uniform (qw = 64 wave)
     const int v0 = l0ok ? l0off - qw * l0stride : FOOB;   // + (qw + 16 qg + s) l0stride
