@@ -76,6 +76,18 @@ def test_collisions_vs_oracle(ea):
     assert oracle.same_bits(got, oracle.forward_interpolate(flow))
 
 
+def test_one_target_holds_everything(ea):
+    """Every pixel moves exactly onto one integer target: its 4 passes all land there (floor = ceil),
+    19,200 contributions in one bucket -- more than a band's list holds, so the banded kernel folds
+    that target by walking the contributions in (pass, point) order."""
+    h, w = 60, 80
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    flow = np.stack([40.0 - xx, 30.0 - yy])[None].astype(np.float32)
+    flow = np.ascontiguousarray(np.repeat(flow, 2, axis=0))
+    got = ea.forward_interpolate_pytorch(_dev(flow)).cpu().numpy()
+    assert oracle.same_bits(got, oracle.forward_interpolate(flow))
+
+
 def test_splat_rejects_cpu_and_bad_shapes(ea):
     with pytest.raises(RuntimeError):
         ea.forward_interpolate_pytorch(torch.zeros(1, 2, 4, 4))

@@ -955,7 +955,7 @@ PATCHES["up_fast"] = PATCHES["up_rcp"] + [("upsample.hip", "            m[k] = e
                                            "            m[k] = __expf(__fsub_rn(m[k], mx));")]
 
 # ---- round 4: the fused lookup + convc1 as the two-workgroup kernel (the tree: warp-specialized)
-PATCHES["mo_2wg"] = [("motion.hip", "constexpr bool kConvWS = true;", "constexpr bool kConvWS = false;")]
+# (mo_2wg: the two-workgroup fused kernel -- the tree since round 5; the WS kernel is lab_patches/lookup_conv_ws.diff)
 
 # ---- round 4: stamps of the warp-specialized fused kernel: per workgroup, the cycles its producer
 # wave 0 spends in produce(), its consumer wave 4 in consume(), both in the barrier, and the steps
@@ -1100,9 +1100,42 @@ PATCHES["soff_full"] = [
     ("build.hip", "__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, voff + uoff, 0, ST_L01);",
      "__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, voff, uoff, ST_L01);")]
 
+# round 5: the split16 GEMM's grouped tile order -- GM m-tiles x all n-tiles per group (tree: 8)
+for _gm in (2, 4, 16):
+    PATCHES[f"gm{_gm}"] = [("build.hip", "    constexpr int GM = 8;\n", f"    constexpr int GM = {_gm};\n")]
+
+# round 5: per-phase stamps of the banded splat (thread 0 of each workgroup, s_memrealtime 100 MHz)
+# -> g_sps[block][0..5] = start, staged, counted, scanned, bucketed, end; ecorr_lab_spstamps()
+SPS_DECL = """
+__device__ unsigned long long g_sps[65536][6];
+__device__ __forceinline__ void sps(int k) {
+    const int id = blockIdx.x + gridDim.x * blockIdx.y;
+    if (threadIdx.x == 0 && id < 65536) g_sps[id][k] = __builtin_amdgcn_s_memrealtime();
+}
+"""
+SPS_EXPORT = """
+extern "C" __attribute__((visibility("default"))) int ecorr_lab_spstamps(void* dst, int n) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ecorr::g_sps), (size_t)n * 48, 0, hipMemcpyDeviceToHost);
+}
+"""
+PATCHES["sp_stamps"] = [
+    ("splat.hip", "constexpr int NTB = 1024;", SPS_DECL + "constexpr int NTB = 1024;"),
+    ("splat.hip", "    const int tid = threadIdx.x, band = blockIdx.x, b = blockIdx.y;\n",
+     "    sps(0);\n    const int tid = threadIdx.x, band = blockIdx.x, b = blockIdx.y;\n"),
+    ("splat.hip", "    __syncthreads();\n    const float* src = staged ? spts : gpts;\n",
+     "    __syncthreads();\n    sps(1);\n    const float* src = staged ? spts : gpts;\n"),
+    ("splat.hip", "    __syncthreads();\n\n    // 2. exclusive scan of cnt[0 .. nb)", "    __syncthreads();\n    sps(2);\n\n    // 2. exclusive scan of cnt[0 .. nb)"),
+    ("splat.hip", "    __syncthreads();\n    // cnt[t] = start of target t's bucket", "    __syncthreads();\n    sps(3);\n    // cnt[t] = start of target t's bucket"),
+    ("splat.hip", "            lkey[lo + r] = k;\n        }\n        __syncthreads();\n",
+     "            lkey[lo + r] = k;\n        }\n        __syncthreads();\n        sps(4);\n"),
+    ("splat.hip", "        for (int t = tid; t < nb; t += NTB) fold_sorted(t, t > 0 ? cnt[t - 1] : 0, cnt[t]);\n        return;\n",
+     "        for (int t = tid; t < nb; t += NTB) fold_sorted(t, t > 0 ? cnt[t - 1] : 0, cnt[t]);\n        __syncthreads();\n        sps(5);\n        return;\n"),
+    ("splat.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + SPS_EXPORT),
+]
+
 
 # recipe-name prefix -> the lab_patches diff it applies on top of
-PREDIFF = {"qs": "build_qs.diff", "lkw_": "lookup_win.diff"}
+PREDIFF = {"qs": "build_qs.diff", "lkw_": "lookup_win.diff", "mo_ws": "lookup_conv_ws.diff"}
 
 
 def build(name):
