@@ -612,6 +612,38 @@ def measure_fp32_step(make_block, coords, B, iters, ideal_s, reps=5):
             "ideal": "fp32-MFMA roof for the build + the lookups at 8 TB/s"}
 
 
+def measure_pack(f1, f2, B, D, H, W, q, stream, reps=20):
+    """The split build's operand pass (pack_both_kernel) alone, after the timed region (whose steps
+    record events around the GEMM only): `reps` back-to-back launches between two HIP events on the
+    launch stream -- kernel boundaries as inside a step, no event between the launches -- per
+    launch, the median of 3 such bursts."""
+    import ctypes
+    import eraft_amd
+    L = eraft_amd._lib.lib()
+    n = ctypes.c_int64()
+    eraft_amd._lib.check(L.ecorr_build_split_workspace_size(B, D, H, W, q, ctypes.byref(n)), "pack ws")
+    ws = torch.empty(n.value, dtype=torch.uint8, device=f1.device)
+    st = eraft_amd._lib.stream_of(f1)
+
+    def launch():
+        eraft_amd._lib.check(L.ecorr_build_split_pack(f1.data_ptr(), f2.data_ptr(), B, D, H, W, q, ws.data_ptr(),
+                                                      st), "pack")
+    for _ in range(3):
+        launch()
+    ts = []
+    for _ in range(3):
+        e0, e1 = timing_event(), timing_event()
+        e0.record(stream)
+        for _ in range(reps):
+            launch()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / reps)
+        e0.destroy()
+        e1.destroy()
+    return sorted(ts)[1]
+
+
 def measure_fp32_build(f1, f2, reps=5, per=3):
     """The fp32-MFMA build (ecorr_build: v_mfma_f32_32x32x2_f32, an exact fmaf chain per element)
     on the same inputs, outside the headline timed region: `per` back-to-back launches into one
@@ -717,8 +749,9 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         evs = [[timing_event() for _ in range(3)] for _ in range(a.steps)]
-        eraft_amd._lib.stage_events = stages = []   # split build: events around its two launches
+        eraft_amd._lib.stage_events = stages = []   # split build: events around its GEMM launch
         eraft_amd._lib.stage_event = timing_event
+        eraft_amd._lib.stage_event_start = not lean   # lean: the operand pass is timed after the loop
         t0 = time.perf_counter()
         for k in range(a.steps):
             step(evs[k], last=k == a.steps - 1)
@@ -729,29 +762,37 @@ def main():
         elapsed = time.perf_counter() - t0
         eraft_amd._lib.stage_events = None
         eraft_amd._lib.stage_event = None
+        eraft_amd._lib.stage_event_start = True
 
     if lean:
         if len(stages) != a.steps:
             raise RuntimeError(f"{len(stages)} split builds recorded for {a.steps} timed steps")
-        build_ms = sum(st[0].elapsed_time(st[2]) for st in stages) / a.steps
-        # step k's lookups: from its GEMM's end to step k + 1's operand pass (the last step: to its
-        # own closing event)
-        ends = [stages[k + 1][0] for k in range(a.steps - 1)] + [evs[-1][2]]
-        look_ms = sum(st[2].elapsed_time(e) for st, e in zip(stages, ends)) / a.steps / iters
-        look_each = [st[2].elapsed_time(e) / iters for st, e in zip(stages, ends)]
-        step_each = [st[0].elapsed_time(e) for st, e in zip(stages, ends)]
+        # two events per timed step, around the GEMM; the operand pass is timed after the loop
+        # (measure_pack) and taken out of the interval from a GEMM's end to the next step's GEMM
+        # start (its 12 lookups + the next operand pass); the last step closes with its own event
+        with torch.no_grad():
+            pack_ms = measure_pack(f1, f2, B, D, H, W, q_local, stream)
+        gemm_each = [e[1].elapsed_time(e[2]) for e in stages]
+        build_ms = sum(gemm_each) / a.steps + pack_ms
+        inter = [stages[k][2].elapsed_time(stages[k + 1][1]) - pack_ms for k in range(a.steps - 1)] + \
+                [stages[-1][2].elapsed_time(evs[-1][2])]
+        look_each = [x / iters for x in inter]
+        look_ms = sum(inter) / a.steps / iters
+        step_each = [g + x + pack_ms for g, x in zip(gemm_each, inter)]
     else:
         build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps
         look_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps / iters
     if not lean:
         look_each = [e[1].elapsed_time(e[2]) / iters for e in evs]
         step_each = [e[0].elapsed_time(e[2]) for e in evs]
-    gemm_each = [e[1].elapsed_time(e[2]) for e in stages] if stages else []
-    pack_ms = sum(e[0].elapsed_time(e[1]) for e in stages) / len(stages) if stages else 0.0
+    if not lean:
+        gemm_each = [e[1].elapsed_time(e[2]) for e in stages] if stages else []
+        pack_ms = sum(e[0].elapsed_time(e[1]) for e in stages) / len(stages) if stages else 0.0
     gemm_ms = sum(e[1].elapsed_time(e[2]) for e in stages) / len(stages) if stages else build_ms
     for ev in evs + stages:
         for e in ev:
-            e.destroy()
+            if e is not None:
+                e.destroy()
     if distributed:
         t = torch.tensor([elapsed, build_ms, look_ms, pack_ms, gemm_ms], dtype=torch.float64,
                          device="cpu" if single else device)
@@ -787,7 +828,9 @@ def main():
                                 other_roof={k: other[k] for k in ("bound", "achieved", "peak", "unit", "frac")},
                                 window={"ms": round(build_ms, 4), "frac": wbind["frac"], "achieved": wbind["achieved"],
                                         "covers": f"pack_both_kernel + {split_kernel} (the whole CorrBlock build)"})
-        kernels["pack"] = {"ms_per_launch": round(pack_ms, 4), "covers": "pack_both_kernel (operand pass)",
+        kernels["pack"] = {"ms_per_launch": round(pack_ms, 4),
+                           "covers": "pack_both_kernel (operand pass)" + (": 20 back-to-back launches between two "
+                                     "events after the timed region, median of 3" if lean else ""),
                            "bound": "hbm", "work_per_launch": f"{4.0 * B * D * (q_local + H * W) * 2:.4g} B "
                                                              "(fmaps in, f16 hi/lo panels out)"}
     else:
@@ -797,9 +840,9 @@ def main():
     kernels["lookup"] = {"bound": "hbm", "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(look_gbs / PEAK_HBM_GBS, 4), "ms_per_launch": round(look_ms, 4),
                          "launches_per_step": iters, "work_per_launch": f"{look_bytes:.4g} B" + note,
-                         "covers": ("a step's 12 lookups / 12, from its GEMM's end event to the next step's "
-                                    "operand-pass event (the last step: its closing event) -- kernel boundaries "
-                                    "and any host gap before the next step's first launch included" if lean else
+                         "covers": ("a step's 12 lookups / 12: from its GEMM's end event to the next step's "
+                                    "GEMM-start event minus the operand pass (kernels.pack; the last step: to its "
+                                    "closing event) -- kernel boundaries and host gaps included" if lean else
                                     "a step's 12 lookups / 12 between two HIP events")}
 
     def spread_seq(xs):   # min / median / max and the first and last of the sequence
@@ -812,8 +855,8 @@ def main():
     # (DESIGN.md §5), so the spread shows where in that transient the driver's steps sit
     kernels["per_step"] = {"steps": a.steps, "step_ms": spread_seq(step_each),
                            "lookup_ms_per_call": spread_seq(look_each),
-                           "covers": "HIP events of the timed region: a step from its operand pass (or build) "
-                                     "to the next step's; lookup = its 12 calls / 12"}
+                           "covers": "HIP events of the timed region (lean: GEMM + its 12 lookups + "
+                                     "kernels.pack); lookup = its 12 calls / 12"}
     if gemm_each:
         kernels["build"]["per_step_ms"] = spread_seq(gemm_each)
     if mode == "split" and a.mode == "batch" and world == 1 and not a.no_next:

@@ -169,9 +169,12 @@ if _build_mode not in BUILD_MODES:
 
 
 # Timing hook (bench.py): when a list, every split build appends its (start, after the operand
-# pass, after the GEMM) HIP events, recorded on the launch stream.  Never changes a result.
+# pass, after the GEMM) HIP events, recorded on the launch stream (start is None unless
+# stage_event_start: bench.py times the operand pass outside its timed region, one event fewer per
+# step -- each costs ~5 us of idle GPU).  Never changes a result.
 stage_events = None
 stage_event = None   # bench.py: the timing-event class for stage_events (default torch.cuda.Event)
+stage_event_start = True
 
 
 def set_build_mode(mode: str):
@@ -201,8 +204,9 @@ def build_pyramid(fmap1, fmap2, B, D, H, W, q_count, levels, off, what, mode=Non
         tm = stage_events
         if tm is not None:   # bench.py: HIP events on this stream around the two stages
             mk = stage_event or (lambda: torch.cuda.Event(enable_timing=True))
-            ev = [mk() for _ in range(3)]
-            ev[0].record()
+            ev = [mk() if stage_event_start else None, mk(), mk()]
+            if ev[0] is not None:
+                ev[0].record()
         check(lib().ecorr_build_split_pack(fmap1.data_ptr(), fmap2.data_ptr(), B, D, H, W, q_count,
                                            ws.data_ptr(), st), what)
         if tm is not None:
