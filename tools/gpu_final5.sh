@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-4 final: every GPU test, smoke, the headline bench + C3 / C5 lines, a 2-rank batch-sharded
+# Round-5 final: every GPU test, smoke, the headline bench + C3 / C5 lines, a 2-rank batch-sharded
 # rehearsal on one GPU (gloo), then the rocprof kernel trace and the PMC passes (C2 full set, C3 /
 # C5 traffic).  usage: tools/gpu_final4.sh TAG
-cd "$GRAFT_REPO_ROOT"; TAG=${1:-r4final}; OUT=gpurun_out/$TAG; mkdir -p $OUT
+cd "$GRAFT_REPO_ROOT"; TAG=${1:-r5final}; OUT=gpurun_out/$TAG; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E 'FAILED|ERROR|passed|failed' $OUT/pytest_gpu.log | tail -8; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1

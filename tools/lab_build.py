@@ -1133,6 +1133,24 @@ PATCHES["sp_stamps"] = [
     ("splat.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + SPS_EXPORT),
 ]
 
+# round 5 diagnostics (timing only): output stores concentrated on 307 KB (the channel term dropped:
+# all 81 channels of a level write one 256-B piece per workgroup) -- do the output writes cost the
+# window reads their cache hits?  And window loads all from the first query group's slab (every
+# workgroup reads the same lines: L2 hits)
+PATCHES["lk_stsmall"] = [("lookup.hip", "sbase + (a * K + bb) * P.q_count * 4, kOutAux);", "sbase * 0 + ((a * K + bb) & 0), kOutAux);")]
+PATCHES["lk_ldsmall"] = [("lookup_stage.h", "    const int64_t R0 = (int64_t)b * P.q_count + q0;   // first query row of the group",
+                          "    const int64_t R0 = 0 * ((int64_t)b * P.q_count + q0);   // (lab: every group reads group 0)")]
+COMBOS["lk_bothsmall"] = ["lk_stsmall", "lk_ldsmall"]
+
+# timing only: each workgroup's 81 channels x 64 queries written as one contiguous 20.7 KB piece
+# (same bytes, same store instructions, a wrong layout) -- does the NCHW output's 256-B-per-row
+# scatter cost the write stream?
+PATCHES["lk_stblock"] = [
+    ("lookup.hip", "    const int voff = p * 4;\n    const int sbase = lv * KK * P.q_count * 4;",
+     "    const int voff = g * 4;\n    const int sbase = (blockIdx.x + gridDim.x * lv) * KK * 256;"),
+    ("lookup.hip", "sbase + (a * K + bb) * P.q_count * 4, kOutAux);", "sbase + (a * K + bb) * 256, kOutAux);"),
+    ("lookup.hip", "sbase + ((part * AP + ai) * K + bb) * P.q_count * 4, kOutAux);", "sbase + ((part * AP + ai) * K + bb) * 256, kOutAux);")]
+
 
 # recipe-name prefix -> the lab_patches diff it applies on top of
 PREDIFF = {"qs": "build_qs.diff", "lkw_": "lookup_win.diff", "mo_ws": "lookup_conv_ws.diff"}
