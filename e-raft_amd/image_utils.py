@@ -25,10 +25,19 @@ def _require_device_f32(name, t):
         raise TypeError(f"{name} must be float32 (got {t.dtype})")
 
 
+_WS_BYTES = {}
+
+
 def _workspace(B, n, h, w, device):
-    nbytes = ctypes.c_int64()
-    _lib.check(_lib.lib().ecorr_splat_workspace_size(B, n, h, w, ctypes.byref(nbytes)), "splat workspace")
-    return torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=device)
+    """The splat's scratch (ecorr_splat_workspace_size), or None when the shape needs none (the banded
+    kernel: n <= 65536 points per item); sizes are cached per shape."""
+    key = (B, n, h, w)
+    nb = _WS_BYTES.get(key)
+    if nb is None:
+        nbytes = ctypes.c_int64()
+        _lib.check(_lib.lib().ecorr_splat_workspace_size(B, n, h, w, ctypes.byref(nbytes)), "splat workspace")
+        nb = _WS_BYTES[key] = nbytes.value
+    return torch.empty(nb, dtype=torch.uint8, device=device) if nb > 0 else None
 
 
 def grid_sample_values(input, height, width):
@@ -45,7 +54,7 @@ def grid_sample_values(input, height, width):
         ws = _workspace(1, n, height, width, dev)
         _lib.check(_lib.lib().ecorr_grid_sample_values(
             pts.data_ptr() if n else None, n, height, width, values.data_ptr(), valid.data_ptr(),
-            ws.data_ptr(), _lib.stream_of(pts)), "grid_sample_values")
+            None if ws is None else ws.data_ptr(), _lib.stream_of(pts)), "grid_sample_values")
     return values, valid
 
 
@@ -64,6 +73,6 @@ def forward_interpolate_pytorch(flow_in):
             return out
         ws = _workspace(b, h * w, h, w, dev)
         _lib.check(_lib.lib().ecorr_forward_interpolate(
-            flow.data_ptr(), b, h, w, out.data_ptr(), ws.data_ptr(), _lib.stream_of(flow)),
+            flow.data_ptr(), b, h, w, out.data_ptr(), None if ws is None else ws.data_ptr(), _lib.stream_of(flow)),
             "forward_interpolate")
     return out

@@ -1151,6 +1151,26 @@ PATCHES["lk_stblock"] = [
     ("lookup.hip", "sbase + (a * K + bb) * P.q_count * 4, kOutAux);", "sbase + (a * K + bb) * 256, kOutAux);"),
     ("lookup.hip", "sbase + ((part * AP + ai) * K + bb) * P.q_count * 4, kOutAux);", "sbase + ((part * AP + ai) * K + bb) * 256, kOutAux);")]
 
+# ---- round 5, split convc1: what bounds conv1x1_split_kernel (timing only)?  Every workgroup reads
+# batch item 0's first 64 query columns (the corr stream served by L2), and / or every output store
+# out of range (no write stream)
+PATCHES["cv_l2ld"] = [("conv.hip", "const_cast<float*>(in + (int64_t)b * C * Q), 0, C * Q * 4, 0x00020000);",
+                       "const_cast<float*>(in + (int64_t)0 * b * C * Q), 0, C * Q * 4, 0x00020000);"),
+                      ("conv.hip", "const int cbase = (qok ? q : C * Q) * 4, qs = Q * 4;",
+                       "const int cbase = (qok ? qi : C * Q) * 4, qs = Q * 4;")]
+PATCHES["cv_stoob"] = [("conv.hip", "const int obase = (qok ? q : O * Q) * 4;", "const int obase = (O * Q + 0 * q) * 4;")]
+COMBOS["cv_bothoob"] = ["cv_l2ld", "cv_stoob"]
+# (the ring form -- column chunks by LDS-DMA from a producer wave that waits only for its own loads
+#  -- was measured from a tree copy and dropped: profiles/r05_lab/cv_ab_ring_oob.txt)
+# query blocks per workgroup (QB: 2 = 64 queries, 4 = 128 queries sharing each weight chunk) and
+# the column prefetch distance; cvq4n: QB 4 without the 4-waves-per-SIMD register cap (1 workgroup/CU)
+for _qb, _pd in [(4, 1), (2, 1), (4, 2)]:
+    PATCHES[f"cvq{_qb}p{_pd}"] = [("conv.hip", "constexpr int kConvQB = 2;", f"constexpr int kConvQB = {_qb};"),
+                                  ("conv.hip", "constexpr int kConvPD = 2;", f"constexpr int kConvPD = {_pd};")]
+PATCHES["cvq4n"] = PATCHES["cvq4p2"] + [("conv.hip", "amdgpu_waves_per_eu(QB > 2 ? 4 : 1)", "amdgpu_waves_per_eu(1)")]
+# timing only: no weight DMA inside the K loop (every chunk multiplies the prologue's stale weights)
+PATCHES["cv_nowdma"] = [("conv.hip", "        issue_w(min(c + 2, nkc - 1), (c + 2) % NB);   // past the last chunk a harmless repeat\n", "")]
+
 
 # recipe-name prefix -> the lab_patches diff it applies on top of
 PREDIFF = {"qs": "build_qs.diff", "lkw_": "lookup_win.diff", "mo_ws": "lookup_conv_ws.diff"}
