@@ -43,6 +43,7 @@ typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef unsigned int uintx4 __attribute__((ext_vector_type(4)));
 
+constexpr int SQ = 64;                 // queries per workgroup
 constexpr int SO = 256;                // output channels per workgroup (8 row blocks of 32)
 constexpr int SNT = 256;               // threads (4 waves)
 constexpr int SKC = 16;                // channels per chunk (one v_mfma_f32_32x32x16_f16 K)
@@ -110,23 +111,19 @@ __device__ __forceinline__ void wait_vm() {
 // The weight chunks go global -> LDS by LDS-DMA (no staging registers; through registers it was
 // 63.9 vs 53.9 us, profiles/r04_lab/r4l_ab_conv.txt), three buffers, two chunks ahead, with static
 // vmcnt waits (tests/test_isa_waits.py replays them on the emitted ISA); the query columns are
-// loaded PD chunks ahead into PD + 1 fixed register sets.  QB query blocks of 32 per workgroup
-// (2 QB waves: wave w owns query block w % QB and channel half w / QB).
-template <int PD, int QB>
-__global__ __launch_bounds__(128 * QB) __attribute__((amdgpu_waves_per_eu(QB > 2 ? 4 : 1))) void conv1x1_split_kernel(const float* __restrict__ in, int C, int Q,
+// loaded PD chunks ahead into PD + 1 fixed register sets.
+template <int PD>
+__global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restrict__ in, int C, int Q,
                                                             const float* __restrict__ qmax, int G,
                                                             const char* __restrict__ packed,
                                                             const float* __restrict__ bias, int O,
                                                             float* __restrict__ out) {
     constexpr int NB = 3;
-    constexpr int NW = 2 * QB, NQ = 32 * QB;   // waves, queries per workgroup
-    constexpr int PPW = 16 / NW;               // 1-KB weight pieces per wave and chunk
-    static_assert(16 % NW == 0, "weight pieces per wave");
     // ALL LDS in one object: with a second __shared__ object hipcc waits vmcnt(0) before every
     // ds_read while an LDS-DMA is in flight (cdna_hip_programming.md, the second-__shared__ trap)
     struct Lds {
         char wbuf[NB][SCHUNK];   // weight chunks
-        float red[2][NQ];        // per-query maxima of the two channel halves
+        float red[2][SQ];        // per-query maxima of the two channel halves
         int sex[SO];             // the block's weight-row exponents
         float sbias[SO];         // and biases (0 past O or without bias)
     };
@@ -135,9 +132,9 @@ __global__ __launch_bounds__(128 * QB) __attribute__((amdgpu_waves_per_eu(QB > 2
     auto& red = sh.red;
     auto& sex = sh.sex;
     auto& sbias = sh.sbias;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, qb = w % QB, oh = w / QB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, qb = w & 1, oh = w >> 1;
     const int ob = blockIdx.y, b = blockIdx.z, nob = gridDim.y, nkc = split_chunks(C);
-    const int qi = 32 * qb + (lane & 31), q = blockIdx.x * NQ + qi, kh = lane >> 5;
+    const int qi = 32 * qb + (lane & 31), q = blockIdx.x * SQ + qi, kh = lane >> 5;
     const bool qok = q < Q;
     // corr / out of batch item b as range-checked buffers: a lane past Q starts at the end of the
     // range (every access then reads 0 / is dropped), channels past C or O fall outside by
@@ -155,16 +152,16 @@ __global__ __launch_bounds__(128 * QB) __attribute__((amdgpu_waves_per_eu(QB > 2
             v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, off + j * qs, 0, 0));
     };
 
-    // wave w copies the chunk's 1-KB pieces w, w + NW, ... (lane-linear, as LDS-DMA writes them), the
-    // chunk offset in the scalar soffset
+    // wave w copies the chunk's 1-KB pieces w, w + 4, w + 8, w + 12 (lane-linear, as LDS-DMA writes
+    // them), the chunk offset in the scalar soffset
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wsrc), 0, nkc * SCHUNK, 0x00020000);
     auto issue_w = [&](int c, int buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int s = 0; s < PPW; ++s)
+        for (int s = 0; s < 4; ++s)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                wrs, (__attribute__((address_space(3))) void*)(wbuf[buf] + (w + NW * s) * 1024), 16,
-                (w + NW * s) * 1024 + lane * 16, c * SCHUNK, 0, 0);
+                wrs, (__attribute__((address_space(3))) void*)(wbuf[buf] + (w + 4 * s) * 1024), 16,
+                (w + 4 * s) * 1024 + lane * 16, c * SCHUNK, 0, 0);
     };
 
     // ---- prologue: every load in flight before the first wait (one memory latency, not five):
@@ -177,11 +174,10 @@ __global__ __launch_bounds__(128 * QB) __attribute__((amdgpu_waves_per_eu(QB > 2
     for (int k = 0; k < PD; ++k) load_b(k, bv[k]);   // past C: out of range, zeros
     // (bias and maxima through range-checked buffers: a null pointer is a 0-byte range reading 0 --
     // no branches, whose merged wait states cost a full drain here)
-    const int to = tid & (SO - 1);   // (threads past SO load a repeat and write nothing)
-    const int eo_t = reinterpret_cast<const int*>(packed + (int64_t)nob * nkc * SCHUNK)[ob * SO + to];
+    const int eo_t = reinterpret_cast<const int*>(packed + (int64_t)nob * nkc * SCHUNK)[ob * SO + tid];
     const __amdgpu_buffer_rsrc_t brs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bias), 0, bias ? O * 4 : 0, 0x00020000);
-    const float bo_t = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (ob * SO + to) * 4, 0, 0));
+    const float bo_t = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (ob * SO + tid) * 4, 0, 0));
     constexpr int QG = 6;   // partial maxima per wave and pass (G = 12 for 4 levels: one pass)
     const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(qmax ? qmax + (int64_t)b * G * Q : nullptr), 0, qmax ? G * Q * 4 : 0, 0x00020000);
@@ -191,10 +187,8 @@ __global__ __launch_bounds__(128 * QB) __attribute__((amdgpu_waves_per_eu(QB > 2
     for (int i = 0; i < QG; ++i)
         qv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(qrs, (min(oh + 2 * i, G - 1) * Q + qc) * 4, 0, 0));
     __builtin_amdgcn_sched_barrier(0);
-    if (NW * 64 <= SO || tid < SO) {
-        sex[to] = eo_t;
-        sbias[to] = bo_t;
-    }
+    sex[tid] = eo_t;
+    sbias[tid] = bo_t;
 
     // ---- the query's largest |value| over C -> its exponent: from the lookup's partial maxima
     // (ecorr_lookup_qmax; clamped repeats are harmless) or a pre-pass over the column
@@ -219,7 +213,7 @@ __global__ __launch_bounds__(128 * QB) __attribute__((amdgpu_waves_per_eu(QB > 2
     m = fmaxf(m, __shfl_xor(m, 32));
     if (kh == 0) red[oh][qi] = m;
     __builtin_amdgcn_sched_barrier(0);
-    wait_vm<PPW + 8 * PD>();   // chunk 0's pieces (chunk 1's PPW and PD x 8 B loads may be in flight)
+    wait_vm<4 + 8 * PD>();   // chunk 0's pieces (chunk 1's 4 and PD x 8 B loads may be in flight)
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): red / sex / sbias written
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -244,23 +238,36 @@ __global__ __launch_bounds__(128 * QB) __attribute__((amdgpu_waves_per_eu(QB > 2
         halfx8 bh, bl;
         split8(cur, sq, bh, bl);
         const char* wb = wbuf[c % NB] + lane * 16;
+        // A fragments double-buffered: tile i + 2's pair is read right after tile i's MFMAs issue, so
+        // the LDS latency hides behind them (read just before use: 55.5 vs 52.0 us at DSEC B = 16,
+        // profiles/r05_lab/cv_ab_adb.txt)
+        halfx8 ah[2], al[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            ah[i] = *reinterpret_cast<const halfx8*>(wb + ((4 * oh + i) * 2 + 0) * 1024);
+            al[i] = *reinterpret_cast<const halfx8*>(wb + ((4 * oh + i) * 2 + 1) * 1024);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int rb = 4 * oh + i;
-            const halfx8 ah = *reinterpret_cast<const halfx8*>(wb + (rb * 2 + 0) * 1024);
-            const halfx8 al = *reinterpret_cast<const halfx8*>(wb + (rb * 2 + 1) * 1024);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[i], 0, 0, 0);
+            const int s = i & 1;
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc[i], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i + 2 < 4) {
+                ah[s] = *reinterpret_cast<const halfx8*>(wb + ((4 * oh + i + 2) * 2 + 0) * 1024);
+                al[s] = *reinterpret_cast<const halfx8*>(wb + ((4 * oh + i + 2) * 2 + 1) * 1024);
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
         // chunk c + 1's pieces landed (only this step's 8 B loads + 4 pieces may be newer) and this
         // wave's reads of chunk c are done (the next step's DMA overwrites it); a bare s_barrier:
         // __syncthreads()'s release fence would wait for every load in flight (vmcnt(0))
         __builtin_amdgcn_sched_barrier(0);
         if (tail)
-            wait_vm<PPW>();   // (stricter than needed if the loads were kept: still correct)
+            wait_vm<4>();   // (stricter than needed if the loads were kept: still correct)
         else
-            wait_vm<8 + PPW>();
+            wait_vm<12>();
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -298,7 +305,6 @@ __global__ __launch_bounds__(128 * QB) __attribute__((amdgpu_waves_per_eu(QB > 2
 }
 
 constexpr int kConvPD = 2;   // query-column prefetch distance (chunks)
-constexpr int kConvQB = 2;   // query blocks of 32 per workgroup
 
 }  // namespace
 
@@ -323,9 +329,9 @@ int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const float*
         (int64_t)(O + split_oblocks(O) * SO) * Q * 4 >= 0x7fffffffLL)
         return ECORR_EINVAL;
     if ((const void*)in == (const void*)out) return ECORR_EINVAL;
-    const dim3 grid((unsigned)((Q + 32 * kConvQB - 1) / (32 * kConvQB)), (unsigned)split_oblocks(O), (unsigned)B);
-    hipLaunchKernelGGL((conv1x1_split_kernel<kConvPD, kConvQB>), grid, dim3(128 * kConvQB), 0, stream, in, C, Q, qmax,
-                       G, (const char*)packed, bias, O, out);
+    const dim3 grid((unsigned)((Q + SQ - 1) / SQ), (unsigned)split_oblocks(O), (unsigned)B);
+    hipLaunchKernelGGL(conv1x1_split_kernel<kConvPD>, grid, dim3(SNT), 0, stream, in, C, Q, qmax, G,
+                       (const char*)packed, bias, O, out);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
 }

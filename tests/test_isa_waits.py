@@ -168,7 +168,7 @@ def test_checker_flags_a_hoisted_query_load(asm):
 # race when the remainder still waited vmcnt(12)).  Its K loop is
 # rolled (3 steps per trip) with a 0-2 step remainder, so the straight-line stream replayed here is
 # prologue + two trips of the loop body + both remainder steps: barriers 0 (prologue) .. 8.
-CONV = "conv1x1_split_kernelILi2ELi2EE"   # <PD, QB>
+CONV = "conv1x1_split_kernelILi2EE"
 
 
 @pytest.fixture(scope="module")

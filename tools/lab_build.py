@@ -1168,12 +1168,33 @@ for _qb, _pd in [(4, 1), (2, 1), (4, 2)]:
     PATCHES[f"cvq{_qb}p{_pd}"] = [("conv.hip", "constexpr int kConvQB = 2;", f"constexpr int kConvQB = {_qb};"),
                                   ("conv.hip", "constexpr int kConvPD = 2;", f"constexpr int kConvPD = {_pd};")]
 PATCHES["cvq4n"] = PATCHES["cvq4p2"] + [("conv.hip", "amdgpu_waves_per_eu(QB > 2 ? 4 : 1)", "amdgpu_waves_per_eu(1)")]
+# (A fragments double-buffered -- cv_adb, profiles/r05_lab/cv_ab_adb.txt -- is in the tree since round 5)
+# timing only: no step barrier (LDS buffers race), or no MFMAs (the A / B
+# operands still read and split, one add each keeps them live)
+PATCHES["cv_nobar_"] = [("conv.hip", """        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };""", """        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+        __builtin_amdgcn_sched_barrier(0);
+    };""")]
+PATCHES["cv_nomfma_"] = [("conv.hip", x, y) for x, y in [
+    ("acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc[i], 0, 0, 0);",
+     "acc[i][0] += (float)ah[s][0] * (float)bl[0] + (float)al[s][1] * (float)bh[1];"),
+    ("acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc[i], 0, 0, 0);", ""),
+    ("acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc[i], 0, 0, 0);", "")]]
+COMBOS["cv_adb_nobar"] = ["cv_nobar_"]
+COMBOS["cv_adb_nomfma"] = ["cv_nomfma_"]
+# 2 tiles per wave: a workgroup covers 128 output channels (half the weight chunk, 2 pieces per
+# wave), 4 workgroups per CU; the halves of a query tile back to back on one XCD
+PATCHES["cvt2"] = [("conv.hip", "constexpr int kConvTPW = 4;", "constexpr int kConvTPW = 2;")]
+PATCHES["cvt2p3"] = PATCHES["cvt2"] + [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 3;")]
 # timing only: no weight DMA inside the K loop (every chunk multiplies the prologue's stale weights)
 PATCHES["cv_nowdma"] = [("conv.hip", "        issue_w(min(c + 2, nkc - 1), (c + 2) % NB);   // past the last chunk a harmless repeat\n", "")]
 
 
 # recipe-name prefix -> the lab_patches diff it applies on top of
-PREDIFF = {"qs": "build_qs.diff", "lkw_": "lookup_win.diff", "mo_ws": "lookup_conv_ws.diff"}
+PREDIFF = {"qs": "build_qs.diff", "lkw_": "lookup_win.diff", "mo_ws": "lookup_conv_ws.diff", "cvq": "conv_tiles.diff",
+           "cvt": "conv_tiles.diff"}
 
 
 def build(name):
