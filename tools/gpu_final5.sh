@@ -39,5 +39,6 @@ for f in sorted(glob.glob(sys.argv[1] + "/bench*.log")):
           k["lookup"]["ms_per_launch"], "traffic", d["roofline"].get("traffic"))
 PY
 # the SURVEY §8f rows (split / fused convc1, upsampling, splat, voxel) under the kernel trace, no e2e
+mkdir -p $OUT/prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof/kt_next -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $OUT/prof/kt_next.log 2>&1
 rc=$?; echo "kt next rc=$rc"; exit $rc
