@@ -9,7 +9,9 @@
 // 2x the mask size.  Here it is one pass: thread = (n, i, pixel p) with lanes on consecutive
 // pixels, so each of its 72 mask loads is a coalesced 256-byte wave row, the 3x3 flow window
 // comes from L1/L2, and the 8 sub-pixels j of a row leave as two float4 stores (a wave writes
-// 64 x 32 contiguous bytes).  HBM-bound: 2304 B of mask in + 512 B of flow out per pixel.
+// 64 x 32 contiguous bytes).  HBM-bound: 2304 B of mask in + 512 B of flow out per pixel.  The mask
+// loads use the default cache policy (non-temporal loads: 42.2 vs 36.7 us at DSEC B = 16,
+// profiles/r05_lab/up_ab_policy.txt); the output stores stay non-temporal.
 //
 // Numerics: softmax as max, exp(x - max), in-order sum, times the sum's reciprocal; then the
 // in-order sum of the 9 products -- the reference's expression order.  exp is the hardware's
@@ -61,7 +63,7 @@ __global__ __launch_bounds__(NTU) void upsample_kernel(const float* __restrict__
     for (int j = 0; j < 8; ++j) {
         float m[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) m[k] = __builtin_nontemporal_load(mrow + ((int64_t)k * 64 + j) * HW);
+        for (int k = 0; k < 9; ++k) m[k] = mrow[((int64_t)k * 64 + j) * HW];   // default policy: 36.7 vs 42.2 us non-temporal
         float mx = m[0];
 #pragma unroll
         for (int k = 1; k < 9; ++k) mx = fmaxf(mx, m[k]);

@@ -1188,6 +1188,26 @@ COMBOS["cv_adb_nomfma"] = ["cv_nomfma_"]
 # wave), 4 workgroups per CU; the halves of a query tile back to back on one XCD
 PATCHES["cvt2"] = [("conv.hip", "constexpr int kConvTPW = 4;", "constexpr int kConvTPW = 2;")]
 PATCHES["cvt2p3"] = PATCHES["cvt2"] + [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 3;")]
+# convex upsampling (upsample.hip): two sub-rows i, i + 4 per thread (the 3x3 flow window loaded once,
+# half the workgroups: one dispatch round at DSEC B = 16); mask loads with the default policy
+PATCHES["up_i2"] = [("upsample.hip", """    const int i = blockIdx.y, n = blockIdx.z;
+    if (p >= HW) return;""", """    const int n = blockIdx.z;
+    if (p >= HW) return;"""),
+                    ("upsample.hip", """    const float* mrow = mask + ((int64_t)n * 576 + i * 8) * HW + p;""",
+                     """#pragma unroll 1
+    for (int i = blockIdx.y; i < 8; i += 4) {
+    const float* mrow = mask + ((int64_t)n * 576 + i * 8) * HW + p;"""),
+                    ("upsample.hip", """        __builtin_nontemporal_store(floatx4{res[c][4], res[c][5], res[c][6], res[c][7]}, (floatx4*)(o + 4));
+    }
+}""", """        __builtin_nontemporal_store(floatx4{res[c][4], res[c][5], res[c][6], res[c][7]}, (floatx4*)(o + 4));
+    }
+    }
+}"""),
+                    ("upsample.hip", "const dim3 grid((unsigned)((H * W + NTU - 1) / NTU), 8, (unsigned)N);",
+                     "const dim3 grid((unsigned)((H * W + NTU - 1) / NTU), 4, (unsigned)N);")]
+PATCHES["up_ldplain"] = [("upsample.hip", "m[k] = __builtin_nontemporal_load(mrow + ((int64_t)k * 64 + j) * HW);",
+                          "m[k] = mrow[((int64_t)k * 64 + j) * HW];")]
+COMBOS["up_i2_ldplain"] = ["up_i2", "up_ldplain"]
 # timing only: no weight DMA inside the K loop (every chunk multiplies the prologue's stale weights)
 PATCHES["cv_nowdma"] = [("conv.hip", "        issue_w(min(c + 2, nkc - 1), (c + 2) % NB);   // past the last chunk a harmless repeat\n", "")]
 
