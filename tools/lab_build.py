@@ -1208,6 +1208,16 @@ PATCHES["up_i2"] = [("upsample.hip", """    const int i = blockIdx.y, n = blockI
 PATCHES["up_ldplain"] = [("upsample.hip", "m[k] = __builtin_nontemporal_load(mrow + ((int64_t)k * 64 + j) * HW);",
                           "m[k] = mrow[((int64_t)k * 64 + j) * HW];")]
 COMBOS["up_i2_ldplain"] = ["up_i2", "up_ldplain"]
+# convex upsampling: output stores with the default policy instead of non-temporal
+PATCHES["up_stplain"] = [("upsample.hip", """        __builtin_nontemporal_store(floatx4{res[c][0], res[c][1], res[c][2], res[c][3]}, (floatx4*)o);
+        __builtin_nontemporal_store(floatx4{res[c][4], res[c][5], res[c][6], res[c][7]}, (floatx4*)(o + 4));""",
+                          """        *(floatx4*)o = floatx4{res[c][0], res[c][1], res[c][2], res[c][3]};
+        *(floatx4*)(o + 4) = floatx4{res[c][4], res[c][5], res[c][6], res[c][7]};""")]
+# lookup: window loads non-temporal (aux 2) -- the upsampling's lesson checked the other way
+PATCHES["lk_ldnt"] = [("lookup_stage.h", "const uint2v u = __builtin_amdgcn_raw_buffer_load_b64(rsrc, need ? off : OOB, 0, 0);",
+                       "const uint2v u = __builtin_amdgcn_raw_buffer_load_b64(rsrc, need ? off : OOB, 0, 2);"),
+                      ("lookup_stage.h", "vals[c][ry][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));",
+                       "vals[c][ry][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 2));")]
 # timing only: no weight DMA inside the K loop (every chunk multiplies the prologue's stale weights)
 PATCHES["cv_nowdma"] = [("conv.hip", "        issue_w(min(c + 2, nkc - 1), (c + 2) % NB);   // past the last chunk a harmless repeat\n", "")]
 
