@@ -55,6 +55,7 @@ def test_grid_sample_values_goldens(ea, splat):
     (64, 32, 32, 1.5),     # MVSEC (configs[2])
     (4, 92, 160, 3.0),     # 1280x720 (configs[4])
     (1, 130, 140, 4.0),    # > 16384 targets: counts in the workspace instead of LDS
+    (1, 264, 300, 3.0),    # > 65536 points: the one-workgroup-per-item kernel and its workspace
     (2, 7, 300, 40.0),     # mostly out of the image
 ])
 def test_forward_interpolate_vs_oracle(ea, B, h, w, sigma):
@@ -86,6 +87,18 @@ def test_one_target_holds_everything(ea):
     flow = np.ascontiguousarray(np.repeat(flow, 2, axis=0))
     got = ea.forward_interpolate_pytorch(_dev(flow)).cpu().numpy()
     assert oracle.same_bits(got, oracle.forward_interpolate(flow))
+
+
+def test_grid_sample_values_many_points_vs_oracle(ea):
+    """> 65536 points: the workspace path (banded kernel only up to 65536 points per item)."""
+    n, h, w = 70_000, 120, 150
+    pts = prng.uniform(7, (3, n), -2.0, 1.0).astype(np.float32)
+    pts[0] = (pts[0] + 2.0) / 3.0 * (w + 1) - 1.0
+    pts[1] = (pts[1] + 2.0) / 3.0 * (h + 1) - 1.0
+    values, valid = ea.grid_sample_values(_dev(pts), h, w)
+    ref_v, ref_m = oracle.grid_sample_values(pts, h, w)
+    assert oracle.same_bits(values.cpu().numpy(), ref_v)
+    assert np.array_equal(valid.cpu().numpy(), ref_m)
 
 
 def test_splat_rejects_cpu_and_bad_shapes(ea):

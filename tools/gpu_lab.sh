@@ -48,6 +48,11 @@ if [ -n "$CV" ]; then   # split convc1 labs, one process
   AB_ALT_LIB=${L#,} timeout -k 10 300 python -u tools/ab_conv.py > $OUT/cv.log 2>&1
   rc=$?; echo "cv rc=$rc"; grep -E "normwise|median" $OUT/cv.log | tail -8; [ $rc -ne 0 ] && exit $rc
 fi
+if [ -n "$STEP" ]; then   # whole-step labs (build + 12 lookups), one process
+  L=""; for n in $STEP; do L="$L,$n=tools/${n}_lab/e-raft_amd/libecorr.so"; done
+  AB_ALT_LIB=${L#,} timeout -k 10 300 python -u tools/ab_step.py > $OUT/step.log 2>&1
+  rc=$?; echo "step rc=$rc"; grep -E "bitwise|median" $OUT/step.log | tail -10; [ $rc -ne 0 ] && exit $rc
+fi
 for n in $MOSTAMPS; do
   timeout -k 10 120 python -u tools/mostamps.py tools/${n}_lab/e-raft_amd/libecorr.so > $OUT/mostamps_$n.log 2>&1
   rc=$?; echo "mostamps $n rc=$rc"; tail -4 $OUT/mostamps_$n.log; [ $rc -ne 0 ] && exit $rc

@@ -1218,6 +1218,28 @@ PATCHES["lk_ldnt"] = [("lookup_stage.h", "const uint2v u = __builtin_amdgcn_raw_
                        "const uint2v u = __builtin_amdgcn_raw_buffer_load_b64(rsrc, need ? off : OOB, 0, 2);"),
                       ("lookup_stage.h", "vals[c][ry][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 0));",
                        "vals[c][ry][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, need ? off : OOB, 0, 2));")]
+# split16 epilogue: levels 2 and 3 (92 + 23 MB at DSEC B = 16, what the 12 lookups re-read most
+# densely) stored with the default policy (or only level 3), so that they may stay in the Infinity
+# Cache for the lookups; levels 0-1 stay nt.  Step-level A/B: tools/ab_step.py
+def _st23(aux, levels):
+    rep = [("build.hip", """    auto fst2 = [&](__amdgpu_buffer_rsrc_t rs, int voff, int uoff, floatx2 v) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, voff + uoff, 0, ST_L01);
+    };""", """    auto fst2 = [&](__amdgpu_buffer_rsrc_t rs, int voff, int uoff, floatx2 v) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, voff + uoff, 0, ST_L01);
+    };
+    auto fst2p = [&](__amdgpu_buffer_rsrc_t rs, int voff, int uoff, floatx2 v) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, voff + uoff, 0, %d);
+    };
+    auto st2p = [&](__amdgpu_buffer_rsrc_t rs, int off, bool ok, floatx2 v) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, ok ? off : SOOB, 0, %d);
+    };""" % (aux, aux))]
+    for lv in levels:
+        rep += [("build.hip", f"if (FULL) fst2(r{lv}, v{lv},", f"if (FULL) fst2p(r{lv}, v{lv},"),
+                ("build.hip", f"else st2(r{lv}, (grp * G{lv}", f"else st2p(r{lv}, (grp * G{lv}")]
+    return rep
+PATCHES["st23_plain"] = _st23(0, (2, 3))
+PATCHES["st3_plain"] = _st23(0, (3,))
+PATCHES["st23_sc1"] = _st23(16, (2, 3))
 # timing only: no weight DMA inside the K loop (every chunk multiplies the prologue's stale weights)
 PATCHES["cv_nowdma"] = [("conv.hip", "        issue_w(min(c + 2, nkc - 1), (c + 2) % NB);   // past the last chunk a harmless repeat\n", "")]
 
