@@ -3,7 +3,7 @@
 #   RUN_TESTS=1 RUN_BENCH=1 AB="name1 name2" ABT="timing-only names" LK="lookup lab names" tools/gpu_lab.sh TAG
 # AB: bitwise-checked build A/Bs (each alone vs the tree); ABT: timing-only build A/Bs (no check);
 # LK: lookup A/Bs (tools/ab_lookup.py, bitwise-checked); STAMPS: build stamps labs (st16*);
-# LKSTAMPS: lookup stamps labs.  Every step under its own time limit,
+# Every step under its own time limit,
 # chained: the first failure ends the call.
 cd "$GRAFT_REPO_ROOT"; TAG=${1:-lab}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
 if [ -n "$LISTCTR" ]; then   # the PMC counters this box offers
@@ -60,11 +60,5 @@ done
 for n in $STAMPS; do   # build stamps labs (tools/stamps16.py)
   timeout -k 10 120 python -u tools/stamps16.py tools/${n}_lab/e-raft_amd/libecorr.so > $OUT/stamps_$n.log 2>&1
   rc=$?; echo "stamps $n rc=$rc"; cat $OUT/stamps_$n.log | tail -7; [ $rc -ne 0 ] && exit $rc
-done
-for n in $LKSTAMPS; do   # lookup stamps (tools/lkstamps.py), smooth and i.i.d. fields
-  for f in smooth iid; do
-    timeout -k 10 120 python -u tools/lkstamps.py tools/${n}_lab/e-raft_amd/libecorr.so $f > $OUT/lkstamps_${n}_$f.log 2>&1
-    rc=$?; echo "lkstamps $n $f rc=$rc"; cat $OUT/lkstamps_${n}_$f.log | tail -12; [ $rc -ne 0 ] && exit $rc
-  done
 done
 exit 0
