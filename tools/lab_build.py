@@ -451,8 +451,10 @@ PATCHES["soff_full"] = [
      "__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, voff, uoff, ST_L01);")]
 
 # round 5: the split16 GEMM's grouped tile order -- GM m-tiles x all n-tiles per group (tree: 8)
+PATCHES["gm16"] = [("build.hip", "    constexpr int GM = 8;\n", "    constexpr int GM = 16;\n")]
+#  the in-kernel clock of each tile-group arm: per-block stamps (tools/stamps16.py)
 for _gm in (2, 4, 16):
-    PATCHES[f"gm{_gm}"] = [("build.hip", "    constexpr int GM = 8;\n", f"    constexpr int GM = {_gm};\n")]
+    COMBOS[f"st16_gm{_gm}"] = ["st16", f"gm{_gm}"]
 
 # round 5: per-phase stamps of the banded splat (thread 0 of each workgroup, s_memrealtime 100 MHz)
 # -> g_sps[block][0..5] = start, staged, counted, scanned, bucketed, end; ecorr_lab_spstamps()
