@@ -88,19 +88,27 @@ __device__ __forceinline__ NTile ntile_of(const BuildParams& P, int nt) {
     return n;
 }
 
-// Grouped tile order: GM m-tiles x all n-tiles per group, so consecutive tiles share panels.
+// Grouped tile order: GM m-tiles x all n-tiles per group, so consecutive tiles share panels.  BAL:
+// the item's m-tiles split into ceil(n_m / GM) groups of (nearly) equal size instead of full groups
+// and a remainder -- at DSEC (19 split16 query tiles) GM 10 makes two groups (10, 9), so every
+// target panel leaves the L2 twice per item instead of three times (8, 8, 3): FETCH -20%, the build
+// 1.3% shorter (profiles/r05_lab/gm_clock_l2_b.txt); 10 query panels (2.5 MB) + the resident
+// blocks' target panels still fit an XCD's 4-MB L2 (GM 16 does not: 4.5 MB, slower).
+template <int GM, bool BAL>
 __device__ __forceinline__ void decode_tile(const BuildParams& P, int t, int n_m, int& b, int& mt, int& nt) {
-    constexpr int GM = 8;
     const int per_b = n_m * P.n_nt;
     b = t / per_b;
     const int i = t - b * per_b;
-    const int gsz = GM * P.n_nt;
+    const int ng = (n_m + GM - 1) / GM;
+    const int gm = BAL ? (n_m + ng - 1) / ng : GM;
+    const int gsz = gm * P.n_nt;
     const int grp = i / gsz, gi = i - grp * gsz;
-    const int first_m = grp * GM;
-    const int gsm = min(n_m - first_m, GM);
+    const int first_m = grp * gm;
+    const int gsm = min(n_m - first_m, gm);
     mt = first_m + gi % gsm;
     nt = gi / gsm;
 }
+constexpr int kGM16 = 10;   // build_split16_kernel's group bound (balanced); the other builds: 8
 
 // One pooled-level pixel (row, col) of a query image: tiled (ntx > 0; the tile must exist, cells
 // in a tile's padding are written and never read), interleaved (ntx < 0; likewise the block) or
@@ -446,7 +454,7 @@ __global__ __launch_bounds__(256, 2) void build_split_kernel(BuildParams P) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int b, qt, nt;
-    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    decode_tile<8, false>(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
     const NTile tc = ntile_of(P, nt);
     const int q0 = qt * SQ;
     const int H = P.H, W = P.W;
@@ -973,7 +981,7 @@ __global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int b, qt, nt;
-    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    decode_tile<kGM16, true>(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
     const NTile tc = ntile_of(P, nt);
     const int q0 = qt * SQ;
     const int H = P.H, W = P.W;
@@ -1170,7 +1178,7 @@ __global__ __launch_bounds__(256, 2) void build_f32_kernel(BuildParams P) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int b, qt, nt;
-    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    decode_tile<8, false>(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
     b = __builtin_amdgcn_readfirstlane(b);
     qt = __builtin_amdgcn_readfirstlane(qt);
     nt = __builtin_amdgcn_readfirstlane(nt);
@@ -1671,7 +1679,7 @@ __global__ __launch_bounds__(NT, 3) void build_kernel(BuildParams P) {
     TileCoord tc;
     {
         int mt, nt;
-        decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_mt, tc.b, mt, nt);
+        decode_tile<8, false>(P, xcd_remap(blockIdx.x, gridDim.x), P.n_mt, tc.b, mt, nt);
         const NTile n = ntile_of(P, nt);
         tc.m0 = mt * BM;
         tc.ty0 = n.ty0;

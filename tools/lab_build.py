@@ -45,8 +45,10 @@ PATCHES["loopprio3"] = [("build.hip", "    TFrags fa, fb;\n", "    __builtin_amd
 PATCHES["lk_noblend"] = [("lookup.hip", "                const float v = blend(c[0], c[1], c[SW], c[SW + 1], wx[ai], wy[bb]);",
                           "                const float v = c[0];")]
 # tile order: m-tiles per group of the grouped order (tree: 8)
-for _gm in (2, 3, 4, 6):
-    PATCHES[f"gm{_gm}"] = [("build.hip", "    constexpr int GM = 8;", f"    constexpr int GM = {_gm};")]
+# split16 tile-group bound (balanced groups since round 5; the round-4/5 records of gm2/4/16 were
+# taken with full groups + a remainder, gm9/10/12 are the same either way at DSEC's 19 query tiles)
+for _gm in (2, 3, 4, 6, 8, 9, 12, 16):
+    PATCHES[f"gm{_gm}"] = [("build.hip", "constexpr int kGM16 = 10;", f"constexpr int kGM16 = {_gm};")]
 # timing only: each v_mfma_f32_32x32x16_f16 replaced by two v_mfma_f32_16x16x32_f16 on the same
 # fragments (the same MAC count, garbage sums): does the 16x16 shape hold a higher clock here?
 def _m16(x, y):
@@ -80,7 +82,7 @@ PATCHES["st16"] = [
     ("build.hip", "constexpr int SQ = 256; ", ST16_DECL + "constexpr int SQ = 256; "),
     ("build.hip", """    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int b, qt, nt;
-    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    decode_tile<kGM16, true>(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
     const NTile tc = ntile_of(P, nt);
     const int q0 = qt * SQ;
     const int H = P.H, W = P.W;
@@ -91,7 +93,7 @@ PATCHES["st16"] = [
     unsigned long long c_mid = 0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int b, qt, nt;
-    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    decode_tile<kGM16, true>(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
     const NTile tc = ntile_of(P, nt);
     const int q0 = qt * SQ;
     const int H = P.H, W = P.W;
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(256, 2) void build_split16_kernel(BuildParams P) {
     int* exq""", """template <bool MUL>
 __device__ __forceinline__ void split16_tile(const BuildParams& P, char* smem, int tile) {
     int* exq"""),
-    ("build.hip", """    decode_tile(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
+    ("build.hip", """    decode_tile<kGM16, true>(P, xcd_remap(blockIdx.x, gridDim.x), P.n_qt, b, qt, nt);
     const NTile tc = ntile_of(P, nt);
     const int q0 = qt * SQ;
     const int H = P.H, W = P.W;
@@ -451,9 +453,9 @@ PATCHES["soff_full"] = [
      "__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, voff, uoff, ST_L01);")]
 
 # round 5: the split16 GEMM's grouped tile order -- GM m-tiles x all n-tiles per group (tree: 8)
-PATCHES["gm16"] = [("build.hip", "    constexpr int GM = 8;\n", "    constexpr int GM = 16;\n")]
+# (GM = 10 in two balanced groups at DSEC -- kept, build.hip decode_tile; gm_clock_l2_b.txt)
 #  the in-kernel clock of each tile-group arm: per-block stamps (tools/stamps16.py)
-for _gm in (2, 4, 16):
+for _gm in (2, 4, 8, 9, 12, 16):
     COMBOS[f"st16_gm{_gm}"] = ["st16", f"gm{_gm}"]
 
 # round 5: per-phase stamps of the banded splat (thread 0 of each workgroup, s_memrealtime 100 MHz)
