@@ -590,6 +590,11 @@ def _st23(aux, levels):
 PATCHES["st23_plain"] = _st23(0, (2, 3))
 PATCHES["st3_plain"] = _st23(0, (3,))
 PATCHES["st23_sc1"] = _st23(16, (2, 3))
+# timing only (phase-1 conflicts): every staging ds_write at a lane-linear,
+# conflict-free address (same instruction count; the windows then hold the wrong values)
+PATCHES["lk_wrlin"] = [("lookup_stage.h",
+    "                    st.win[sr.skip[c] == v ? DUMMY : sr.dst[c] + ry * SW + v] = sr.vals[c][ry][v];",
+    "                    st.win[(((c * SR::S + ry) * SR::V + v) * NTQ + (int)threadIdx.x % NTQ) % DUMMY] = sr.vals[c][ry][v];")]
 # timing only: no weight DMA inside the K loop (every chunk multiplies the prologue's stale weights)
 PATCHES["cv_nowdma"] = [("conv.hip", "        issue_w(min(c + 2, nkc - 1), (c + 2) % NB);   // past the last chunk a harmless repeat\n", "")]
 
