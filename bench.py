@@ -17,6 +17,10 @@ One step = one pass of the hot path over one batch: CorrBlock build (split-f16 o
     python bench.py [--gpus N --steps K --warmup W --batch 16 --no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 
+`--gpus N` always means N ranks: without a launcher (no WORLD_SIZE in the environment) and N > 1,
+bench.py starts torch.distributed.run with N processes as a child and forwards its JSON line and
+exit code; under a launcher whose WORLD_SIZE differs from N it exits non-zero.
+
 Prints ONE JSON line on rank 0 with `roofline` (the dominant kernel, the split GEMM alone --
 build_split16_kernel at D = 256 --
 HIP events on its launch stream inside the timed region; `window_frac` = the whole build with its
@@ -703,8 +707,36 @@ def measure_fp32_build(f1, f2, reps=5, per=3):
                     "tests/test_build_modes_gpu.py)"}
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` (N > 1) with no launcher around it: start N ranks under
+    torch.distributed.run as a CHILD process (never exec -- this process has not touched the GPU,
+    but the ranks will) and return its exit code; rank 0's single JSON line reaches our stdout
+    through the inherited descriptor."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    sys.stdout.flush()
+    return subprocess.run(cmd, cwd=ROOT).returncode
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        raise SystemExit(f"--gpus {a.gpus}: need at least one rank")
+    if "WORLD_SIZE" not in os.environ:
+        if a.gpus > 1:   # before any GPU call in this process
+            raise SystemExit(launch_ranks(a.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: launch N ranks "
+                         f"for --gpus N (or run `python bench.py --gpus N` alone and it launches them)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -26,21 +26,33 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_two_rank_batch_shard():
+def _gpu_untouched():
     # Precondition: this process has not initialised the GPU.  The launcher is a forked child of
     # the pytest process; a child that execs from a GPU-initialised parent can take the machine
-    # down on this pool.  conftest.py orders this test first in the session; if a reordering ever
-    # runs a GPU test before it, fail here instead of spawning the ranks.
+    # down on this pool.  conftest.py orders these tests first in the session; if a reordering ever
+    # runs a GPU test before them, fail here instead of spawning the ranks.
     torch = sys.modules.get("torch")
     if torch is not None and torch.cuda.is_initialized():
-        pytest.fail("test_two_rank_batch_shard must run before any test initialises the GPU in this "
-                    "process (conftest.py puts it first); run it alone: pytest tests/test_batch_shard_gpu.py")
+        pytest.fail("the spawning tests must run before any test initialises the GPU in this "
+                    "process (conftest.py puts them first); run alone: pytest tests/test_batch_shard_gpu.py")
+
+
+@pytest.mark.parametrize("launcher", ["bench_itself", "torchrun"])
+def test_two_rank_batch_shard(launcher):
+    """`bench_itself`: `python bench.py --gpus 2` with no launcher around it -- the form a driver
+    may run for its 1/2/4/8 curve -- must start the 2 ranks itself."""
+    _gpu_untouched()
     steps, B = 2, 16
     env = dict(os.environ, BENCH_SINGLE_DEVICE="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", str(steps), "--warmup", "1",
-           "--batch", str(B), "--no-next", "--no-cpu-baseline"]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    bench = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", str(steps), "--warmup", "1",
+             "--batch", str(B), "--no-next", "--no-cpu-baseline"]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + bench
+    else:
+        cmd = [sys.executable] + bench
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
