@@ -230,7 +230,8 @@ __global__ __launch_bounds__(NTB) void splat_band_kernel(SplatArgs A, int G) {
     __shared__ int wsum[NTB / kWave];
     __shared__ int nlist, carry_s;
     __shared__ int sub[kBandTargets + 1];   // sub-range boundaries (overflow path)
-    const int tid = threadIdx.x, band = blockIdx.x, b = blockIdx.y;
+    // one linear block index (band fastest): no gridDim.y limit on the batch (B > 65535 launches)
+    const int tid = threadIdx.x, band = (int)(blockIdx.x % (unsigned)G), b = (int)(blockIdx.x / (unsigned)G);
     const int n = (int)A.n, hw = A.h * A.w;
     const int t0 = (int)((int64_t)band * hw / G), t1 = (int)((int64_t)(band + 1) * hw / G), nb = t1 - t0;
     const float* gpts = A.pts + (int64_t)b * NP * n;
@@ -508,8 +509,10 @@ int launch_splat(bool flow_mode, const float* pts, int B, int64_t n, int h, int 
     A.ws_keys = ws ? ws + (hw > kLdsTargets ? (int64_t)B * hw : 0) : nullptr;
     if (band_mode(n)) {
         const int G = band_count(B, hw);
-        if (flow_mode) hipLaunchKernelGGL((splat_band_kernel<true>), dim3(G, B), dim3(NTB), 0, stream, A, G);
-        else hipLaunchKernelGGL((splat_band_kernel<false>), dim3(G, B), dim3(NTB), 0, stream, A, G);
+        if ((int64_t)G * B > 0x7fffffff) return ECORR_EINVAL;
+        const dim3 grid((unsigned)(G * B));
+        if (flow_mode) hipLaunchKernelGGL((splat_band_kernel<true>), grid, dim3(NTB), 0, stream, A, G);
+        else hipLaunchKernelGGL((splat_band_kernel<false>), grid, dim3(NTB), 0, stream, A, G);
         return hip_status();
     }
     const bool lds = lds_mode(flow_mode, n, hw);

@@ -108,3 +108,14 @@ def test_splat_rejects_cpu_and_bad_shapes(ea):
         ea.forward_interpolate_pytorch(torch.zeros(1, 3, 4, 4, device="cuda"))
     with pytest.raises(RuntimeError):
         ea.grid_sample_values(torch.zeros(2, 5, device="cuda"), 4, 4)
+
+
+def test_batch_past_grid_y_limit(ea):
+    """the banded splat once put the batch on gridDim.y (limit 65535); with a linear block
+    index a batch of 65,600 small maps runs, and every item equals the same item splatted alone."""
+    B, h, w = 65600, 3, 4
+    g = torch.Generator(device="cuda").manual_seed(11)
+    flow = (torch.randn((B, 2, h, w), generator=g, device="cuda") * 1.5).contiguous()
+    out = ea.forward_interpolate_pytorch(flow)
+    for i in (0, 1, 65534, 65535, 65536, B - 1):
+        assert torch.equal(out[i:i + 1], ea.forward_interpolate_pytorch(flow[i:i + 1].contiguous())), i
