@@ -436,7 +436,14 @@ def measure_voxel(device, n=1_000_000, C=15, H=480, W=640, reps=5):
     torch_ref.voxel_grid_dsec(evc, C, H, W)
     ref_cpu = (time.perf_counter() - t0) * 1e3
     torch.set_num_threads(nt)
+    # algorithmic bytes: the four event fields in (fp32) + the grid out, once each
+    nbytes = 16.0 * n + 4.0 * C * H * W
+    gbs = nbytes / (ours * 1e-3) / 1e9
     return {"ms_per_call": round(ours, 4), "events": n, "grid": [C, H, W],
+            "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "work_per_launch": f"{nbytes:.4g} B (events in + grid out; the counting sort's key-range passes "
+                               "and the ordered gather are not algorithmic bytes)",
             "events_per_s": round(n / (ours * 1e-3), 1),
             "reference_ops_on_gpu_ms": round(ref_gpu, 3), "reference_ops_on_1_cpu_core_ms": round(ref_cpu, 1),
             "speedup_vs_reference_gpu": round(ref_gpu / ours, 2),
@@ -901,6 +908,10 @@ def main():
                                     "GEMM-start event minus the operand pass (kernels.pack; the last step: to its "
                                     "closing event) -- kernel boundaries and host gaps included" if lean else
                                     "a step's 12 lookups / 12 between two HIP events")}
+    if lean:   # the lookup share is an estimate (the pack burst-timed after the loop)
+        kernels["lookup"]["estimate"] = ("pack-subtracted: kernels.pack is timed in warm back-to-back bursts "
+                                         "after the timed region, not inside each step; tools/lk_percall.py "
+                                         "times each call between its own events")
 
     def spread_seq(xs):   # min / median / max and the first and last of the sequence
         if not xs:
@@ -913,7 +924,7 @@ def main():
     kernels["per_step"] = {"steps": a.steps, "step_ms": spread_seq(step_each),
                            "lookup_ms_per_call": spread_seq(look_each),
                            "covers": "HIP events of the timed region (lean: GEMM + its 12 lookups + "
-                                     "kernels.pack); lookup = its 12 calls / 12"}
+                                     "kernels.pack, a pack-subtracted estimate); lookup = its 12 calls / 12"}
     if gemm_each:
         kernels["build"]["per_step_ms"] = spread_seq(gemm_each)
     if mode == "split" and a.mode == "batch" and world == 1 and not a.no_next:

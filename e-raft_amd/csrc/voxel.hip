@@ -10,12 +10,14 @@
 //   prep    per event: the reference's fp32/fp64 arithmetic up to the base cell key (the cell its
 //           pass-0 corner lands in; DSEC keys live on a grid extended by one cell on the low side
 //           because x0 = -1 still reaches x = 0) and the per-event factors the weights need;
-//   bucket  counting sort by key: per-key counts (integer atomics, in prep), exclusive scan
-//           (reduce -> scan of the tile sums -> tile scans), events dropped into their key's run
-//           (integer atomics pick the slot);
-//   order   per key, its run insertion-sorted by event index (runs are short and the atomics
-//           hand out slots nearly in event order, so this is ~linear) and the events' weight
-//           factors gathered once into run order (one float4 each);
+//   bucket  counting sort by key: per event its arrival rank in its key (one returning integer
+//           atomic, in prep), exclusive scan of the counts (reduce -> scan of the tile sums ->
+//           tile scans, 16-byte loads and stores), each event and its weight factors (one float4)
+//           dropped at run start + rank -- no second atomic pass (round 6: the two random-atomic
+//           passes were 96 of the 282 us per DSEC window, profiles/r06_lab);
+//   order   per key with two or more events, its run insertion-sorted by event index (runs are
+//           short and the atomics hand out ranks nearly in event order, so this is ~linear) and
+//           the run's weight factors re-gathered into that order;
 //   gather  per target cell, the runs of the base cells its 8 (DSEC) / 2 (MVSEC) passes read, in
 //           pass order, each in event order: the reference's fold, bit for bit.  Neighbouring
 //           cells read neighbouring runs, so the payload reads are near-contiguous.  With
@@ -55,8 +57,9 @@ struct VoxelArgs {
     int C, H, W;
     uint32_t K;           // key range; key K = no contribution
     uint32_t* key;        // per event: base-cell key (K = none)
-    uint32_t* cnt;        // per key: event count (zeroed), then
-    uint32_t* off;        // per key: exclusive offset, after the fill the run end (start = off[k-1])
+    uint32_t* rank;       // per event: its arrival rank among its key's events (atomic order)
+    uint32_t* cnt;        // per key: event count (K + 1 entries, zeroed; cnt[K] stays 0)
+    uint32_t* off;        // per key: exclusive offset = run start; off[K] = the runs' total
     int* slot;            // run order: event index
     float *fa, *fb;       // DSEC: t_norm, value; MVSEC: left, right (0 when the right pass is masked)
     float4* payload;      // sorted order: DSEC (x, y, t_norm, value); MVSEC (left, right, -, -)
@@ -77,7 +80,7 @@ __global__ __launch_bounds__(NTV) void prep_dsec(VoxelArgs A) {
     const bool in = x0 >= -1 && x0 < A.W && y0 >= -1 && y0 < A.H && ti >= -1 && ti < A.C;
     const uint32_t k = in ? (uint32_t)(((int64_t)(ti + 1) * (A.H + 1) + (y0 + 1)) * (A.W + 1) + (x0 + 1)) : A.K;
     A.key[e] = k;
-    if (in) atomicAdd(&A.cnt[k], 1u);
+    if (in) A.rank[e] = atomicAdd(&A.cnt[k], 1u);
     A.fa[e] = tn;
     A.fb[e] = __fsub_rn(__fmul_rn(2.0f, A.p[e]), 1.0f);   // :41 value = 2*p - 1
 }
@@ -103,39 +106,53 @@ __global__ __launch_bounds__(NTV) void prep_mvsec(VoxelArgs A) {
     if ((vl && (idx < 0 || idx >= CHW)) || (vr && (idx + HW < 0 || idx + HW >= CHW))) atomicOr(A.bad, 1);
     const bool ok = vl && idx >= 0 && idx < CHW;
     A.key[e] = ok ? (uint32_t)idx : A.K;
-    if (ok) atomicAdd(&A.cnt[idx], 1u);
+    if (ok) A.rank[e] = atomicAdd(&A.cnt[idx], 1u);
     A.fa[e] = __fmul_rn(pol, __fsub_rn(1.0f, dts));           // :96 vals_left
     A.fb[e] = vr ? __fmul_rn(pol, dts) : 0.0f;                 // :97 vals_right (+0: a no-op add)
 }
 
-// Drop every event into its key's run; off[k] walks from the run start to the next run's start.
+template <bool DSEC>
+__device__ __forceinline__ float4 payload_of(const VoxelArgs& A, int64_t e) {
+    return DSEC ? make_float4(A.x[e], A.y[e], A.fa[e], A.fb[e]) : make_float4(A.fa[e], A.fb[e], 0.0f, 0.0f);
+}
+
+// Drop every event and its weight factors at its run's start + its rank (event-parallel: the
+// event fields are read coalesced, no atomics).
+template <bool DSEC>
 __global__ __launch_bounds__(NTV) void fill_runs(VoxelArgs A) {
     const int64_t e = blockIdx.x * (int64_t)NTV + threadIdx.x;
     if (e >= A.n) return;
     const uint32_t k = A.key[e];
-    if (k < A.K) A.slot[atomicAdd(&A.off[k], 1u)] = (int)e;
+    if (k >= A.K) return;
+    const uint32_t i = A.off[k] + A.rank[e];
+    A.slot[i] = (int)e;
+    A.payload[i] = payload_of<DSEC>(A, e);
 }
 
 __device__ __forceinline__ uint2 run_of(const VoxelArgs& A, int64_t k) {
-    return make_uint2(k > 0 ? A.off[k - 1] : 0u, A.off[k]);
+    return make_uint2(A.off[k], A.off[k + 1]);
 }
 
-// Per key: order its run by event index, then gather the events' weight factors into run order.
+// Per run of two or more events (found by its rank-1 event: event-parallel, 1M threads at DSEC
+// instead of one per key, 4.9M): order it by event index, then re-gather its weight factors into
+// that order (a one-event run is already in place).
 template <bool DSEC>
 __global__ __launch_bounds__(NTV) void order_runs(VoxelArgs A) {
-    const int64_t k = blockIdx.x * (int64_t)NTV + threadIdx.x;
-    if (k >= A.K) return;
+    const int64_t e = blockIdx.x * (int64_t)NTV + threadIdx.x;
+    if (e >= A.n) return;
+    const uint32_t k = A.key[e];
+    if (k >= A.K || A.rank[e] != 1u) return;
     const uint2 r = run_of(A, k);
+    bool moved = false;
     for (uint32_t i = r.x + 1; i < r.y; ++i) {
         const int v = A.slot[i];
         uint32_t j = i;
         while (j > r.x && A.slot[j - 1] > v) { A.slot[j] = A.slot[j - 1]; --j; }
         A.slot[j] = v;
+        moved |= j != i;
     }
-    for (uint32_t i = r.x; i < r.y; ++i) {
-        const int e = A.slot[i];
-        A.payload[i] = DSEC ? make_float4(A.x[e], A.y[e], A.fa[e], A.fb[e]) : make_float4(A.fa[e], A.fb[e], 0.0f, 0.0f);
-    }
+    if (moved)
+        for (uint32_t i = r.x; i < r.y; ++i) A.payload[i] = payload_of<DSEC>(A, A.slot[i]);
 }
 
 // (count, mean, M2) of a set of values; Chan et al.'s pairwise combination, in double.
@@ -165,44 +182,80 @@ __device__ __forceinline__ Moments block_moments(Moments m, double* sh) {
     return {sh[0], sh[1], sh[2]};
 }
 
+// Block = a contiguous range of grid rows (tc, yc); its threads walk the range's cells in order,
+// 256 apart, with (row, xc) stepped incrementally (no per-cell integer division; every lane busy
+// whatever W is); the keys of a cell's 8 passes are the row's base key + xc minus constants
+// (32-bit: the key range is < 2^32), and lanes on consecutive xc read consecutive run bounds.
 template <bool DSEC>
 __global__ __launch_bounds__(NTV) void gather(VoxelArgs A, int normalize) {
     __shared__ double sh[3 * NTV];
-    const int64_t HW = (int64_t)A.H * A.W, cells = HW * A.C;
-    Moments mom{0.0, 0.0, 0.0};   // this thread's nonzero cells, folded in cell order
-    for (int64_t cell = blockIdx.x * (int64_t)NTV + threadIdx.x; cell < cells; cell += (int64_t)gridDim.x * NTV) {
-        float acc = 0.0f;
-        if (DSEC) {
-            const int tc = (int)(cell / HW), rem = (int)(cell - tc * HW), yc = rem / A.W, xc = rem - yc * A.W;
-            const float fx = (float)xc, fy = (float)yc, ft = (float)tc;
-            // dsec_utils.py:43-45 pass order: xlim outer, ylim, tlim inner
+    const int rows = A.C * A.H;
+    const int per = (rows + gridDim.x - 1) / gridDim.x;
+    const int r0 = blockIdx.x * per, r1 = min(rows, r0 + per);
+    // this thread's nonzero cells as plain fp64 sums (no division per cell), turned into (count,
+    // mean, M2) once before the block's fixed-order Chan tree
+    double cn = 0.0, cs = 0.0, css = 0.0;
+    const uint32_t dB = (uint32_t)A.W + 1, dC = ((uint32_t)A.H + 1) * dB;
+    int r = r0 + (int)threadIdx.x / A.W, xc = (int)threadIdx.x % A.W;
+    int tc = r / A.H, yc = r - tc * A.H;
+    for (; r < r1;) {
+        {
+            float acc = 0.0f;
+            if (DSEC) {
+                const float fx = (float)xc, fy = (float)yc, ft = (float)tc;
+                // the pass-0 corner's base key (tc, yc, xc) on the extended grid
+                const uint32_t k0 = ((uint32_t)(tc + 1) * ((uint32_t)A.H + 1) + (uint32_t)(yc + 1)) * dB + (uint32_t)xc + 1;
+                // dsec_utils.py:43-45 pass order: xlim outer, ylim, tlim inner; base key of pass
+                // (a, b, c) = k0 - a - b dB - c dC.  All run bounds first (a = 0 and a = 1 are
+                // adjacent keys: three consecutive offsets per (b, c)), then the folds in order.
+                uint32_t o3[4][3];
 #pragma unroll
-            for (int pass = 0; pass < 8; ++pass) {
-                const int a = pass >> 2, b = (pass >> 1) & 1, c = pass & 1;
-                const int64_t k = ((int64_t)(tc - c + 1) * (A.H + 1) + (yc - b + 1)) * (A.W + 1) + (xc - a + 1);
-                const uint2 run = run_of(A, k);
-                for (uint32_t j = run.x; j < run.y; ++j) {
-                    const float4 ev = A.payload[j];
-                    // :48 value * (1 - |xlim - x|) * (1 - |ylim - y|) * (1 - |tlim - t_norm|), left to right
-                    float wgt = __fmul_rn(ev.w, __fsub_rn(1.0f, fabsf(__fsub_rn(fx, ev.x))));
-                    wgt = __fmul_rn(wgt, __fsub_rn(1.0f, fabsf(__fsub_rn(fy, ev.y))));
-                    wgt = __fmul_rn(wgt, __fsub_rn(1.0f, fabsf(__fsub_rn(ft, ev.z))));
-                    acc = __fadd_rn(acc, wgt);
+                for (int bc = 0; bc < 4; ++bc) {
+                    const uint32_t k1 = k0 - 1u - (uint32_t)(bc >> 1) * dB - (uint32_t)(bc & 1) * dC;   // a = 1
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) o3[bc][i] = A.off[k1 + i];
                 }
-            }
-        } else {
-            // transformers.py:103-113: all left contributions, then all right ones (+W*H)
-            const uint2 rl = run_of(A, cell);
-            for (uint32_t j = rl.x; j < rl.y; ++j) acc = __fadd_rn(acc, A.payload[j].x);
-            if (cell >= HW) {
-                const uint2 rr = run_of(A, cell - HW);
+#pragma unroll
+                for (int pass = 0; pass < 8; ++pass) {
+                    const int aa = pass >> 2, bc = pass & 3;
+                    for (uint32_t j = o3[bc][1 - aa]; j < o3[bc][2 - aa]; ++j) {
+                        const float4 ev = A.payload[j];
+                        // :48 value * (1 - |xlim - x|) * (1 - |ylim - y|) * (1 - |tlim - t_norm|), left to right
+                        float wgt = __fmul_rn(ev.w, __fsub_rn(1.0f, fabsf(__fsub_rn(fx, ev.x))));
+                        wgt = __fmul_rn(wgt, __fsub_rn(1.0f, fabsf(__fsub_rn(fy, ev.y))));
+                        wgt = __fmul_rn(wgt, __fsub_rn(1.0f, fabsf(__fsub_rn(ft, ev.z))));
+                        acc = __fadd_rn(acc, wgt);
+                    }
+                }
+            } else {
+                // transformers.py:103-113: all left contributions, then all right ones (+W*H)
+                const int64_t cell = (int64_t)r * A.W + xc, HW = (int64_t)A.H * A.W;
+                const uint2 rl = run_of(A, cell);
+                const uint2 rr = tc > 0 ? run_of(A, cell - HW) : make_uint2(0u, 0u);
+                for (uint32_t j = rl.x; j < rl.y; ++j) acc = __fadd_rn(acc, A.payload[j].x);
                 for (uint32_t j = rr.x; j < rr.y; ++j) acc = __fadd_rn(acc, A.payload[j].y);
             }
+            A.voxel[(int64_t)r * A.W + xc] = acc;
+            if (normalize && acc != 0.0f) {
+                const double v = (double)acc;
+                cn += 1.0;
+                cs += v;
+                css = fma(v, v, css);
+            }
         }
-        A.voxel[cell] = acc;
-        if (normalize && acc != 0.0f) mom = combine(mom, {1.0, (double)acc, 0.0});
+        xc += NTV;   // next cell of this thread: 256 further in row-major order
+        while (xc >= A.W) {
+            xc -= A.W;
+            ++r;
+            if (++yc == A.H) { yc = 0; ++tc; }
+        }
     }
     if (normalize) {   // uniform over the grid
+        Moments mom{0.0, 0.0, 0.0};
+        if (cn > 0.0) {
+            const double mean = cs / cn;
+            mom = {cn, mean, fmax(css - cs * mean, 0.0)};
+        }
         const Moments m = block_moments(mom, sh);
         if (threadIdx.x == 0) {
             A.part[3 * blockIdx.x] = m.n;
@@ -268,13 +321,28 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
     return pre + x - v;
 }
 
-__global__ __launch_bounds__(NTV) void scan_reduce(const uint32_t* __restrict__ in, uint32_t K, uint32_t* __restrict__ sums) {
+// A thread's SCAN_PER consecutive counts: four 16-byte loads (the arrays are 256-byte aligned), the
+// range's tail element by element.
+__device__ __forceinline__ void load16(const uint32_t* __restrict__ in, int64_t base, int64_t K, uint32_t (&v)[SCAN_PER]) {
+    if (base + SCAN_PER <= K) {
+#pragma unroll
+        for (int q = 0; q < SCAN_PER / 4; ++q) {
+            const uint4 u = reinterpret_cast<const uint4*>(in + base)[q];
+            v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_PER; ++k) v[k] = base + k < K ? in[base + k] : 0u;
+    }
+}
+
+__global__ __launch_bounds__(NTV) void scan_reduce(const uint32_t* __restrict__ in, int64_t K, uint32_t* __restrict__ sums) {
     __shared__ uint32_t sh[NTV / 64];
     const int64_t base = (int64_t)blockIdx.x * SCAN_T + threadIdx.x * SCAN_PER;
-    uint32_t v = 0;
+    uint32_t w[SCAN_PER], v = 0;
+    load16(in, base, K, w);
 #pragma unroll
-    for (int k = 0; k < SCAN_PER; ++k)
-        if (base + k < K) v += in[base + k];
+    for (int k = 0; k < SCAN_PER; ++k) v += w[k];
     uint32_t total;
     block_exclusive_scan(v, sh, total);
     if (threadIdx.x == 0) sums[blockIdx.x] = total;
@@ -293,22 +361,30 @@ __global__ __launch_bounds__(NTV) void scan_sums(uint32_t* __restrict__ sums, in
     }
 }
 
-__global__ __launch_bounds__(NTV) void scan_apply(const uint32_t* __restrict__ in, uint32_t K, const uint32_t* __restrict__ sums,
+__global__ __launch_bounds__(NTV) void scan_apply(const uint32_t* __restrict__ in, int64_t K, const uint32_t* __restrict__ sums,
                                                   uint32_t* __restrict__ out) {
     __shared__ uint32_t sh[NTV / 64];
     const int64_t base = (int64_t)blockIdx.x * SCAN_T + threadIdx.x * SCAN_PER;
     uint32_t v[SCAN_PER], s = 0;
+    load16(in, base, K, v);
 #pragma unroll
-    for (int k = 0; k < SCAN_PER; ++k) {
-        v[k] = base + k < K ? in[base + k] : 0;
-        s += v[k];
-    }
+    for (int k = 0; k < SCAN_PER; ++k) s += v[k];
     uint32_t total;
     uint32_t run = sums[blockIdx.x] + block_exclusive_scan(s, sh, total);
+    uint32_t o[SCAN_PER];
 #pragma unroll
     for (int k = 0; k < SCAN_PER; ++k) {
-        if (base + k < K) out[base + k] = run;
+        o[k] = run;
         run += v[k];
+    }
+    if (base + SCAN_PER <= K) {
+#pragma unroll
+        for (int q = 0; q < SCAN_PER / 4; ++q)
+            reinterpret_cast<uint4*>(out + base)[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_PER; ++k)
+            if (base + k < K) out[base + k] = o[k];
     }
 }
 
@@ -318,25 +394,28 @@ inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // Workspace carve-up (every piece 256-byte aligned).
 struct VoxelWs {
-    size_t key, cnt, off, slot, fa, fb, payload, norm, part, scan_sums, total;
+    size_t key, rank, cnt, off, slot, fa, fb, payload, norm, part, scan_sums, total;
 };
 
-constexpr int kGatherBlocks = 2048;   // grid-stride gather: this many normalization partials
+// grid-stride gather: this many blocks (normalization partials); one cell per thread (18,000
+// blocks at DSEC) was slower, 88 vs 75 us, and its 18,000 partials cost the one-block finalize 31 us
+constexpr int kGatherBlocks = 2048;
 
 int plan(int64_t n, uint32_t K, int64_t cells, VoxelWs* w) {
     (void)cells;
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t at = o; o += align256(bytes); return at; };
     w->key = take(4 * (size_t)n);
-    w->cnt = take(4 * (size_t)K);
-    w->off = take(4 * (size_t)K);
+    w->rank = take(4 * (size_t)n);
+    w->cnt = take(4 * ((size_t)K + 1));
+    w->off = take(4 * ((size_t)K + 1));
     w->slot = take(4 * (size_t)n);
     w->fa = take(4 * (size_t)n);
     w->fb = take(4 * (size_t)n);
     w->payload = take(16 * (size_t)n);
     w->norm = take(sizeof(NormState));
     w->part = take(3 * 8 * (size_t)kGatherBlocks);
-    w->scan_sums = take(4 * (((size_t)K + SCAN_T - 1) / SCAN_T));
+    w->scan_sums = take(4 * (((size_t)K + 1 + SCAN_T - 1) / SCAN_T));
     w->total = o;
     return ECORR_OK;
 }
@@ -372,6 +451,7 @@ int launch_voxel(bool dsec, const float* p, const float* t, const float* x, cons
     if (st != ECORR_OK) return st;
     char* base = (char*)workspace;
     A.key = (uint32_t*)(base + w.key);
+    A.rank = (uint32_t*)(base + w.rank);
     A.cnt = (uint32_t*)(base + w.cnt);
     A.off = (uint32_t*)(base + w.off);
     A.slot = (int*)(base + w.slot);
@@ -383,23 +463,26 @@ int launch_voxel(bool dsec, const float* p, const float* t, const float* x, cons
     A.bad = bad;
     NormState* ns = (NormState*)(base + w.norm);
 
-    hipError_t e = hipMemsetAsync(A.cnt, 0, 4 * (size_t)A.K, stream);
+    // (the whole 256-byte-aligned piece: one aligned fill instead of body + tail)
+    hipError_t e = hipMemsetAsync(A.cnt, 0, align256(4 * ((size_t)A.K + 1)), stream);
     if (e != hipSuccess) return ECORR_EHIP - (int)e;
     if (dsec) hipLaunchKernelGGL(prep_dsec, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
     else hipLaunchKernelGGL(prep_mvsec, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
     if ((st = hip_status()) != ECORR_OK) return st;
-    {
-        const unsigned nb = (unsigned)(((size_t)A.K + SCAN_T - 1) / SCAN_T);
+    {   // exclusive scan over K + 1 counts (cnt[K] = 0): off[K] = the runs' total
+        const int64_t K1 = (int64_t)A.K + 1;
+        const unsigned nb = (unsigned)((K1 + SCAN_T - 1) / SCAN_T);
         uint32_t* sums = (uint32_t*)(base + w.scan_sums);
-        hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(NTV), 0, stream, A.cnt, A.K, sums);
+        hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(NTV), 0, stream, A.cnt, K1, sums);
         hipLaunchKernelGGL(scan_sums, dim3(1), dim3(NTV), 0, stream, sums, (int)nb);
-        hipLaunchKernelGGL(scan_apply, dim3(nb), dim3(NTV), 0, stream, A.cnt, A.K, sums, A.off);
+        hipLaunchKernelGGL(scan_apply, dim3(nb), dim3(NTV), 0, stream, A.cnt, K1, sums, A.off);
         if ((st = hip_status()) != ECORR_OK) return st;
     }
-    hipLaunchKernelGGL(fill_runs, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
-    if (dsec) hipLaunchKernelGGL(order_runs<true>, dim3(blocks_for(A.K)), dim3(NTV), 0, stream, A);
-    else hipLaunchKernelGGL(order_runs<false>, dim3(blocks_for(A.K)), dim3(NTV), 0, stream, A);
-    const unsigned gblocks = (unsigned)std::min<int64_t>(kGatherBlocks, blocks_for(cells));
+    if (dsec) hipLaunchKernelGGL(fill_runs<true>, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
+    else hipLaunchKernelGGL(fill_runs<false>, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
+    if (dsec) hipLaunchKernelGGL(order_runs<true>, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
+    else hipLaunchKernelGGL(order_runs<false>, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
+    const unsigned gblocks = (unsigned)std::min<int64_t>(kGatherBlocks, (int64_t)C * H);
     if (dsec) hipLaunchKernelGGL(gather<true>, dim3(gblocks), dim3(NTV), 0, stream, A, normalize);
     else hipLaunchKernelGGL(gather<false>, dim3(gblocks), dim3(NTV), 0, stream, A, normalize);
     if ((st = hip_status()) != ECORR_OK) return st;

@@ -232,6 +232,13 @@ for _sl in (2, 6, 16):
                               f"ok ? base + (int)(s * lsz * 4) : SOOB, 0, ST_L01);\n        __builtin_amdgcn_s_sleep({_sl});\n")]
 COMBOS = {}
 COMBOS.update({"sameqt": ["sameq", "samet"]})
+# round 6, timing only: the store stream kept, every panel AND per-pixel exponent
+# read from batch item 0's first tiles (L2-resident), so the K loop's reads never leave the L2
+PATCHES["sameex"] = [("build.hip", "eq = q0 + tid < P.q_count ? P.ex1[(int64_t)b * P.q_count + q0 + tid] : 0;",
+                      "eq = q0 + tid < P.q_count ? P.ex1[tid] : 0;"),
+                     ("build.hip", "et = (y < H && x < W) ? P.ex2[(int64_t)b * Q + (int64_t)y * W + x] : 0;",
+                      "et = (y < H && x < W) ? P.ex2[tid] : 0;")]
+COMBOS.update({"l2rd": ["sameq", "samet", "sameex"]})
 COMBOS.update({"dmaqoob": ["dmaoob", "qoob"], "noepi_r2": ["noepi"]})
 COMBOS.update({"st16_prio_loop": ["st16", "prio_loop"]})
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"]})
@@ -399,6 +406,19 @@ PATCHES["lk_lvminor"] = [("lookup.hip", _LK_OLD, """    const int lin = blockIdx
 PATCHES["lk_lvmajor"] = _lk_lvmajor(False)
 PATCHES["lk_lvmajor_rev"] = _lk_lvmajor(True)
 PATCHES["cv_pf3"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 3;")]
+# round 6: the query-column loads with the channel row in the scalar soffset (one address VGPR for
+# all 8 loads of a chunk instead of a v_add each); the range rule (an access iff voffset < records
+# and voffset + soffset < records) keeps lanes past Q and channels past C reading 0
+PATCHES["cv_soff"] = [("conv.hip", """        const int off = cbase + (c * SKC + 8 * kh) * qs;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, off + j * qs, 0, 0));""",
+                       """#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, cvo, (c * SKC + j) * qs, 0));"""),
+                      ("conv.hip", "    const int cbase = (qok ? q : C * Q) * 4, qs = Q * 4;\n",
+                       "    const int cbase = (qok ? q : C * Q) * 4, qs = Q * 4;\n    const int cvo = cbase + 8 * kh * qs;\n")]
+COMBOS["cv_soff_pf3"] = ["cv_soff", "cv_pf3"]
 PATCHES["cv_pf4"] = [("conv.hip", "constexpr int kConvPD = 2;", "constexpr int kConvPD = 4;")]
 
 # ---- round 5: is the lookup concurrency-bound?  LDS padded so that 4 / 3 workgroups fit a CU
@@ -474,8 +494,8 @@ extern "C" __attribute__((visibility("default"))) int ecorr_lab_spstamps(void* d
 """
 PATCHES["sp_stamps"] = [
     ("splat.hip", "constexpr int NTB = 1024;", SPS_DECL + "constexpr int NTB = 1024;"),
-    ("splat.hip", "    const int tid = threadIdx.x, band = blockIdx.x, b = blockIdx.y;\n",
-     "    sps(0);\n    const int tid = threadIdx.x, band = blockIdx.x, b = blockIdx.y;\n"),
+    ("splat.hip", "    const int tid = threadIdx.x, band = (int)(blockIdx.x % (unsigned)G), b = (int)(blockIdx.x / (unsigned)G);\n",
+     "    sps(0);\n    const int tid = threadIdx.x, band = (int)(blockIdx.x % (unsigned)G), b = (int)(blockIdx.x / (unsigned)G);\n"),
     ("splat.hip", "    __syncthreads();\n    const float* src = staged ? spts : gpts;\n",
      "    __syncthreads();\n    sps(1);\n    const float* src = staged ? spts : gpts;\n"),
     ("splat.hip", "    __syncthreads();\n\n    // 2. exclusive scan of cnt[0 .. nb)", "    __syncthreads();\n    sps(2);\n\n    // 2. exclusive scan of cnt[0 .. nb)"),

@@ -9,6 +9,13 @@ for grp in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e > $OUT/pmc$i.log 2>&1
   rc=$?; echo "pmc pass $i ($grp) rc=$rc"; [ $rc -ne 0 ] && { tail -5 $OUT/pmc$i.log; exit $rc; }
 done
-for k in conv1x1_split_kernel lookup_conv_kernel upsample_kernel splat_band_kernel voxel lookup_cols_reg; do
+for k in conv1x1_split_kernel lookup_conv_kernel upsample_kernel splat_band_kernel lookup_cols_reg; do
   echo "== $k"; python3 tools/pmc_one.py --summary $OUT $k
 done
+# the voxel grid's ten kernels (their names carry no "voxel": prep_dsec, scan_*, fill_runs, ...),
+# from a probe that runs only them
+for grp in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 120 rocprofv3 --pmc $grp -d $OUT/vox_$grp -o run --output-format csv -- python3 tools/prof_voxel.py 5 > $OUT/vox_$grp.log 2>&1
+  rc=$?; echo "voxel pmc $grp rc=$rc"; [ $rc -ne 0 ] && { tail -5 $OUT/vox_$grp.log; exit $rc; }
+done
+echo "== voxel (per convert call)"; python3 tools/prof_voxel.py --summary $OUT

@@ -30,8 +30,9 @@ _lib._lib = L
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 g = torch.Generator(device="cuda").manual_seed(0)
 with torch.no_grad():
-    f1 = torch.randn((16, 256, 60, 80), generator=g, device="cuda")
-    f2 = torch.randn((16, 256, 60, 80), generator=g, device="cuda")
+    shape = tuple(int(v) for v in os.environ.get("PMC_SHAPE", "16,256,60,80").split(","))   # B,D,H,W
+    f1 = torch.randn(shape, generator=g, device="cuda")
+    f2 = torch.randn(shape, generator=g, device="cuda")
     for _ in range(n):
         eraft_amd.CorrBlock(f1, f2)
     torch.cuda.synchronize()
