@@ -148,6 +148,11 @@ int ecorr_lookup_conv1x1_relu_packed(const float* pyramid, const float* coords, 
  * query's largest |in| itself, one extra pass over in) or float[B][G][Q] partial maxima whose max
  * over g is max_c |in[b][c][p]| (fmaxf semantics, NaN ignored) -- what ecorr_lookup_qmax writes
  * with G = 3 * levels; the result is bitwise the same either way.
+ * Non-finite input (the contract, tests/test_conv_split_gpu.py): a single +-inf or NaN value in a
+ * query column in[b][.][p] makes EVERY output out[b][.][p] of that query NaN (the split's lo half
+ * of an inf is inf - inf), where the reference's fp32 conv + ReLU gives +-inf / 0 / NaN per output;
+ * the other queries are unaffected.  The split CorrBlock build never produces +-inf samples; the
+ * fused entry (ecorr_lookup_conv1x1_relu_packed, fp32 sums) keeps the reference's pattern.
  * Replaces: F.relu(self.convc1(corr)) (update.py:67,74). */
 int ecorr_conv1x1_split_size(int O, int C, int64_t* bytes);
 int ecorr_conv1x1_split_pack(const float* weight, int O, int C, void* packed, void* stream);

