@@ -239,6 +239,20 @@ PATCHES["sameex"] = [("build.hip", "eq = q0 + tid < P.q_count ? P.ex1[(int64_t)b
                      ("build.hip", "et = (y < H && x < W) ? P.ex2[(int64_t)b * Q + (int64_t)y * W + x] : 0;",
                       "et = (y < H && x < W) ? P.ex2[tid] : 0;")]
 COMBOS.update({"l2rd": ["sameq", "samet", "sameex"]})
+# round 6, timing only: the level-0 stores of FULL tiles into one contiguous 128-KB region per block
+# (l0contig: a wave's 8 stores of a query group fill 8 KB; l0c1k: each store instruction writes 1 KB
+# contiguous) instead of 2 x 256 B per query image -- is the scattered write stream's DRAM page
+# locality (row activations, power) part of the GEMM's clock loss?  The pyramid is wrong (AB_NOCHECK).
+_L0C_DECL = ("build.hip", "    const int grpw = qwu >> 6;   // FULL: the wave's interleaved group (block-relative)\n",
+             "    const int grpw = qwu >> 6;   // FULL: the wave's interleaved group (block-relative)\n"
+             "    const __amdgpu_buffer_rsrc_t r0c = __builtin_amdgcn_make_buffer_rsrc(P.lvl[0], 0, 0x7ffffff0, 0x00020000);\n"
+             "    const int c0 = (int)(blockIdx.x * 131072u) + (qwu >> 6) * 4 * 8192 + L0C_LANE;\n")
+PATCHES["l0contig"] = [("build.hip", "constexpr int SQ = 256; ", "#define L0C_LANE ((8 * jl) * 128 + 16 * pc)\nconstexpr int SQ = 256; "), _L0C_DECL,
+                       ("build.hip", "            if (FULL) fst4(r0, v0, (qwu + 16 * qg + s) * l0stride, x);",
+                        "            if (FULL) fst4(r0c, c0 + qg * 8192 + s * 128, 0, x);")]
+PATCHES["l0c1k"] = [("build.hip", "constexpr int SQ = 256; ", "#define L0C_LANE (jl * 128 + 16 * pc)\nconstexpr int SQ = 256; "), _L0C_DECL,
+                    ("build.hip", "            if (FULL) fst4(r0, v0, (qwu + 16 * qg + s) * l0stride, x);",
+                     "            if (FULL) fst4(r0c, c0 + qg * 8192 + s * 1024, 0, x);")]
 COMBOS.update({"dmaqoob": ["dmaoob", "qoob"], "noepi_r2": ["noepi"]})
 COMBOS.update({"st16_prio_loop": ["st16", "prio_loop"]})
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"]})
