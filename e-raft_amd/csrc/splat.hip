@@ -212,8 +212,9 @@ __global__ __launch_bounds__(NTS) void splat_kernel(SplatArgs A) {
 //   4. per target: insertion-sort the bucket, fold in ascending key order = the reference's serial
 //      (pass, point) order, bit for bit, divide.
 // Points are staged in LDS when they fit.  A band whose contributions exceed the list's capacity is
-// served in sub-ranges of targets (re-evaluating the contributions per sub-range); a single target
-// holding more than the capacity is folded by one thread walking the contributions in key order.
+// served in sub-ranges of targets (re-evaluating the contributions per sub-range, buckets ordered by
+// rank as in step 3); a single target holding more than the capacity is folded by one wave walking
+// the contributions in key order.
 // ============================================================================================
 constexpr int NTB = 1024;            // threads per band workgroup
 constexpr int kBandCap = 6144;       // listed contributions per band (LDS)
@@ -339,20 +340,14 @@ __global__ __launch_bounds__(NTB) void splat_band_kernel(SplatArgs A, int G) {
     // cnt[t] = start of target t's bucket, cnt[nb] = the band's total
 
     float* vout = A.values + (int64_t)b * NZ * hw;
-    // 4. (per target) order a bucket keys[lo, hi) and fold it, or (huge) fold target t by walking
-    // every contribution in key order
-    auto fold = [&](int t, int lo, int hi) {
+    // 4. per target: fold its bucket, already in key order (sorted[lo, hi)), or (huge) fold target t
+    // by walking every contribution in key order
+    auto fold_sorted = [&](const int* sorted, int t, int lo, int hi) {
         float acc[NZ], wacc = 0.0f;
 #pragma unroll
         for (int c = 0; c < NZ; ++c) acc[c] = 0.0f;
-        for (int i = lo + 1; i < hi; ++i) {
-            const int k = keys[i];
-            int j = i - 1;
-            while (j >= lo && keys[j] > k) { keys[j + 1] = keys[j]; --j; }
-            keys[j + 1] = k;
-        }
         for (int i = lo; i < hi; ++i) {
-            const int e = keys[i];
+            const int e = sorted[i];
             float x, y, z[NZ], wgt = 0.0f;
             point<FLOW>(src, n, A.w, rcp_w, e & ((1 << kPassShift) - 1), x, y, z);
             target_of(e >> kPassShift, x, y, A.h, A.w, wgt);
@@ -365,37 +360,34 @@ __global__ __launch_bounds__(NTB) void splat_band_kernel(SplatArgs A, int G) {
         for (int c = 0; c < NZ; ++c) vout[c * hw + t0 + t] = __fdiv_rn(acc[c], den);
         if (A.valid) A.valid[(int64_t)b * hw + t0 + t] = wacc > 0.0f;
     };
-    auto fold_sorted = [&](int t, int lo, int hi) {   // lkey[lo, hi): the bucket in key order
-        float acc[NZ], wacc = 0.0f;
-#pragma unroll
-        for (int c = 0; c < NZ; ++c) acc[c] = 0.0f;
-        for (int i = lo; i < hi; ++i) {
-            const int e = lkey[i];
-            float x, y, z[NZ], wgt = 0.0f;
-            point<FLOW>(src, n, A.w, rcp_w, e & ((1 << kPassShift) - 1), x, y, z);
-            target_of(e >> kPassShift, x, y, A.h, A.w, wgt);
-#pragma unroll
-            for (int c = 0; c < NZ; ++c) acc[c] = __fadd_rn(acc[c], __fmul_rn(z[c], wgt));
-            wacc = __fadd_rn(wacc, wgt);
-        }
-        const float den = __fadd_rn(wacc, 1e-15f);   // :44 values_ipl / (weights_acc + 1e-15)
-#pragma unroll
-        for (int c = 0; c < NZ; ++c) vout[c * hw + t0 + t] = __fdiv_rn(acc[c], den);
-        if (A.valid) A.valid[(int64_t)b * hw + t0 + t] = wacc > 0.0f;
-    };
-    auto fold_walk = [&](int t) {   // one thread: every contribution in (pass, point) order
+    // one wave (one thread walking 4n contributions took 3.4 ms at DSEC): its lanes
+    // evaluate 64 consecutive contributions of a pass at once, then the hits are folded one after
+    // another in lane (= point) order from the lanes' products -- the serial fold, bit for bit
+    auto fold_walk = [&](int t) {
+        const int lane = __lane_id();
         float acc[NZ], wacc = 0.0f;
 #pragma unroll
         for (int c = 0; c < NZ; ++c) acc[c] = 0.0f;
         for (int pass = 0; pass < 4; ++pass)
-            for (int s = 0; s < n; ++s) {
-                float x, y, z[NZ], wgt;
-                point<FLOW>(src, n, A.w, rcp_w, s, x, y, z);
-                if (target_of(pass, x, y, A.h, A.w, wgt) != t0 + t) continue;
+            for (int s0 = 0; s0 < n; s0 += kWave) {
+                const int s = s0 + lane;
+                float term[NZ], wgt = 0.0f;
+                bool hit = false;
+                if (s < n) {
+                    float x, y, z[NZ];
+                    point<FLOW>(src, n, A.w, rcp_w, s, x, y, z);
+                    hit = target_of(pass, x, y, A.h, A.w, wgt) == t0 + t;
 #pragma unroll
-                for (int c = 0; c < NZ; ++c) acc[c] = __fadd_rn(acc[c], __fmul_rn(z[c], wgt));
-                wacc = __fadd_rn(wacc, wgt);
+                    for (int c = 0; c < NZ; ++c) term[c] = __fmul_rn(z[c], wgt);
+                }
+                for (uint64_t m = __builtin_amdgcn_ballot_w64(hit); m; m &= m - 1) {
+                    const int l = (int)__builtin_ctzll(m);
+#pragma unroll
+                    for (int c = 0; c < NZ; ++c) acc[c] = __fadd_rn(acc[c], __shfl(term[c], l, kWave));
+                    wacc = __fadd_rn(wacc, __shfl(wgt, l, kWave));
+                }
             }
+        if (lane != 0) return;
         const float den = __fadd_rn(wacc, 1e-15f);
 #pragma unroll
         for (int c = 0; c < NZ; ++c) vout[c * hw + t0 + t] = __fdiv_rn(acc[c], den);
@@ -422,7 +414,7 @@ __global__ __launch_bounds__(NTB) void splat_band_kernel(SplatArgs A, int G) {
             lkey[lo + r] = k;
         }
         __syncthreads();
-        for (int t = tid; t < nb; t += NTB) fold_sorted(t, t > 0 ? cnt[t - 1] : 0, cnt[t]);
+        for (int t = tid; t < nb; t += NTB) fold_sorted(lkey, t, t > 0 ? cnt[t - 1] : 0, cnt[t]);
         return;
     }
     // overflow: sub-ranges [sub[r], sub[r + 1]) of targets holding <= kBandCap contributions each,
@@ -444,7 +436,7 @@ __global__ __launch_bounds__(NTB) void splat_band_kernel(SplatArgs A, int G) {
         const int a = sub[r], e = sub[r + 1];
         const int base = cnt[a];
         if (cnt[e] - base > kBandCap) {   // one target (e = a + 1) beyond the capacity
-            if (tid == 0) fold_walk(a);
+            if (tid < kWave) fold_walk(a);
             __syncthreads();
             continue;
         }
@@ -457,11 +449,25 @@ __global__ __launch_bounds__(NTB) void splat_band_kernel(SplatArgs A, int G) {
 #pragma unroll
             for (int pass = 0; pass < 4; ++pass) {
                 const int t = target_of(pass, x, y, A.h, A.w, wgt) - t0;
-                if (t >= a && t < e) keys[atomicAdd(&lkey[t - a], 1)] = pass << kPassShift | s;
+                if (t >= a && t < e) {
+                    const int slot = atomicAdd(&lkey[t - a], 1);
+                    keys[slot] = pass << kPassShift | s;
+                    ltgt[slot] = t;
+                }
             }
         }
         __syncthreads();
-        for (int t = a + tid; t < e; t += NTB) fold(t, cnt[t] - base, cnt[t + 1] - base);
+        // order each bucket by rank, as the main path (an insertion sort per bucket on one
+        // thread cost O(k^2) serial LDS steps -- 178 ms per call on the collision map)
+        for (int i = tid; i < cnt[e] - base; i += NTB) {
+            const int t = ltgt[i], k = keys[i];
+            const int lo = cnt[t] - base, hi = cnt[t + 1] - base;
+            int rk = 0;
+            for (int j = lo; j < hi; ++j) rk += keys[j] < k;
+            stgt[lo + rk] = k;
+        }
+        __syncthreads();
+        for (int t = a + tid; t < e; t += NTB) fold_sorted(stgt, t, cnt[t] - base, cnt[t + 1] - base);
         __syncthreads();
     }
 }
