@@ -46,4 +46,7 @@ rc=$?; echo "kt next rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 python -u tools/prof_splat_overflow.py > $OUT/splat_overflow.json 2> $OUT/splat_overflow.err
 rc=$?; echo "splat overflow rc=$rc"; cat $OUT/splat_overflow.json; [ $rc -ne 0 ] && exit $rc
 bash tools/pmc_next.sh $TAG/pmcnext > $OUT/pmc_next.txt 2>&1
-rc=$?; echo "pmc next rc=$rc"; tail -25 $OUT/pmc_next.txt; exit $rc
+rc=$?; echo "pmc next rc=$rc"; tail -25 $OUT/pmc_next.txt
+# keep what comes back under gpurun's 64 MiB: the summaries stay, the raw per-dispatch CSVs go
+find $OUT -name '*counter_collection.csv' -delete; find $OUT -name '*kernel_trace.csv' -delete
+exit $rc
