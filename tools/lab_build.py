@@ -257,6 +257,34 @@ COMBOS.update({"dmaqoob": ["dmaoob", "qoob"], "noepi_r2": ["noepi"]})
 COMBOS.update({"st16_prio_loop": ["st16", "prio_loop"]})
 COMBOS.update({"noepi_mfma16": ["noepi", "mfma16"]})
 COMBOS.update({"st16_sscale": ["st16", "sscale"], "st16_noscale": ["st16", "noscale"]})
+# round 6: the round-3 split16 ablations, rebuilt on today's kernel (their recipes were retired; the
+# older noepi / l01oob patch the 32x32 build_split_kernel, not split16): every epilogue store out of
+# range (same instructions, no store traffic), and the epilogue replaced by one store per lane
+PATCHES["s16_stoob"] = [
+    ("build.hip", "__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), rs, ok ? off : SOOB, 0, ST_L01);",
+     "__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), rs, (ok ? off : SOOB) | 0x70000000, 0, ST_L01);"),
+    ("build.hip", "__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, ok ? off : SOOB, 0, ST_L01);",
+     "__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, (ok ? off : SOOB) | 0x70000000, 0, ST_L01);"),
+    ("build.hip", "__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), rs, voff + uoff, 0, ST_L01);",
+     "__builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), rs, (voff + uoff) | 0x70000000, 0, ST_L01);"),
+    ("build.hip", "__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, voff + uoff, 0, ST_L01);",
+     "__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uint2v, v), rs, (voff + uoff) | 0x70000000, 0, ST_L01);")]
+PATCHES["s16_noepi"] = [("build.hip", """    if (q0 + SQ <= P.q_count && (((int64_t)b * P.q_count + q0) & (kGroup - 1)) == 0)
+        split16_epilogue<MUL, true>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+    else
+        split16_epilogue<MUL, false>(P, acc, smem + wave * (2 * 64 * S16LS), wave * 64, exq, ext, fst, tc, b, q0, lane);
+}""", """    {
+        float s = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) s += acc[g][t][i];
+        P.lvl[0][(int64_t)blockIdx.x * 256 + tid] = s;
+    }
+}""")]
+COMBOS.update({"st16_s16stoob": ["st16", "s16_stoob"]})
 
 # ---- round 4: the split16 epilogue's scaling (bitwise-equal variants unless marked timing only)
 _S16_PK = """                for (int h = 0; h < 2; ++h) {
@@ -516,8 +544,8 @@ PATCHES["sp_stamps"] = [
     ("splat.hip", "    __syncthreads();\n    // cnt[t] = start of target t's bucket", "    __syncthreads();\n    sps(3);\n    // cnt[t] = start of target t's bucket"),
     ("splat.hip", "            lkey[lo + r] = k;\n        }\n        __syncthreads();\n",
      "            lkey[lo + r] = k;\n        }\n        __syncthreads();\n        sps(4);\n"),
-    ("splat.hip", "        for (int t = tid; t < nb; t += NTB) fold_sorted(t, t > 0 ? cnt[t - 1] : 0, cnt[t]);\n        return;\n",
-     "        for (int t = tid; t < nb; t += NTB) fold_sorted(t, t > 0 ? cnt[t - 1] : 0, cnt[t]);\n        __syncthreads();\n        sps(5);\n        return;\n"),
+    ("splat.hip", "        for (int t = tid; t < nb; t += NTB) fold_sorted(lkey, t, t > 0 ? cnt[t - 1] : 0, cnt[t]);\n        return;\n",
+     "        for (int t = tid; t < nb; t += NTB) fold_sorted(lkey, t, t > 0 ? cnt[t - 1] : 0, cnt[t]);\n        __syncthreads();\n        sps(5);\n        return;\n"),
     ("splat.hip", "}  // namespace ecorr\n", "}  // namespace ecorr\n" + SPS_EXPORT),
 ]
 
