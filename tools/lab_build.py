@@ -285,6 +285,20 @@ PATCHES["s16_noepi"] = [("build.hip", """    if (q0 + SQ <= P.q_count && (((int6
     }
 }""")]
 COMBOS.update({"st16_s16stoob": ["st16", "s16_stoob"]})
+# round 6: the accumulators in AGPRs ("+a"): the partner block's epilogue VALU then shares no
+# register-file traffic with the MFMAs' accumulator reads / writes; the epilogue pays one
+# v_accvgpr_read per accumulator (bitwise the same pyramid)
+PATCHES["s16_agpr"] = [
+    ("build.hip", """        for (int t = 0; t < 8; ++t) asm volatile("" : "+v"(acc[g][t]));
+
+    // query fragments""", """        for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(acc[g][t]));
+
+    // query fragments"""),
+    ("build.hip", """asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(bq));""",
+     """asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(bq));"""),
+    ("build.hip", """        for (int t = 0; t < 8; ++t) asm volatile("" : "+v"(acc[g][t]));
+    // FULL""", """        for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(acc[g][t]));
+    // FULL""")]
 
 # ---- round 4: the split16 epilogue's scaling (bitwise-equal variants unless marked timing only)
 _S16_PK = """                for (int h = 0; h < 2; ++h) {
