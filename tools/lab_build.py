@@ -285,6 +285,22 @@ PATCHES["s16_noepi"] = [("build.hip", """    if (q0 + SQ <= P.q_count && (((int6
     }
 }""")]
 COMBOS.update({"st16_s16stoob": ["st16", "s16_stoob"]})
+# round 6: the level-0 LDS transpose reads of a query group issued back to back (eight in flight)
+# before its eight stores; the emitted code read two ahead with a wait per store (bitwise the same)
+PATCHES["s16_rd8"] = [("build.hip", """#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const floatx4 x = *reinterpret_cast<const floatx4*>(xr + (s + 8 * jl) * S16LS + 16 * pc);
+            if (FULL) fst4(r0, v0, (qwu + 16 * qg + s) * l0stride, x);
+            else st4(r0, l0off + (16 * qg + s) * l0stride, l0ok && l0q + 16 * qg + s < nq, x);
+        }""", """        floatx4 xs8[8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) xs8[s] = *reinterpret_cast<const floatx4*>(xr + (s + 8 * jl) * S16LS + 16 * pc);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            if (FULL) fst4(r0, v0, (qwu + 16 * qg + s) * l0stride, xs8[s]);
+            else st4(r0, l0off + (16 * qg + s) * l0stride, l0ok && l0q + 16 * qg + s < nq, xs8[s]);
+        }""")]
 # round 6: the accumulators in AGPRs ("+a"): the partner block's epilogue VALU then shares no
 # register-file traffic with the MFMAs' accumulator reads / writes; the epilogue pays one
 # v_accvgpr_read per accumulator (bitwise the same pyramid)
