@@ -301,6 +301,21 @@ PATCHES["s16_rd8"] = [("build.hip", """#pragma unroll
             if (FULL) fst4(r0, v0, (qwu + 16 * qg + s) * l0stride, xs8[s]);
             else st4(r0, l0off + (16 * qg + s) * l0stride, l0ok && l0q + 16 * qg + s < nq, xs8[s]);
         }""")]
+# round 6, timing only (what bounds the split conv's instruction floor?): the split VALU replaced
+# by one conversion per value (lo = 0), and the A-fragment LDS reads replaced by register values
+PATCHES["cv_nosplit"] = [("conv.hip", """        const float x = v[j] * s;
+        const _Float16 h = (_Float16)x;
+        hi[j] = h;
+        lo[j] = (_Float16)(x - (float)h);""", """        hi[j] = (_Float16)v[j];
+        lo[j] = (_Float16)s;""")]
+PATCHES["cv_nolds"] = [("conv.hip", """            ah[i] = *reinterpret_cast<const halfx8*>(wb + ((4 * oh + i) * 2 + 0) * 1024);
+            al[i] = *reinterpret_cast<const halfx8*>(wb + ((4 * oh + i) * 2 + 1) * 1024);""",
+                        """            ah[i] = bh * (_Float16)(i + 1);
+            al[i] = bl * (_Float16)(i + 2);"""),
+                       ("conv.hip", """                ah[s] = *reinterpret_cast<const halfx8*>(wb + ((4 * oh + i + 2) * 2 + 0) * 1024);
+                al[s] = *reinterpret_cast<const halfx8*>(wb + ((4 * oh + i + 2) * 2 + 1) * 1024);""",
+                        """                ah[s] = bl * (_Float16)(i + 3);
+                al[s] = bh * (_Float16)(i + 4);""")]
 # round 6: the accumulators in AGPRs ("+a"): the partner block's epilogue VALU then shares no
 # register-file traffic with the MFMAs' accumulator reads / writes; the epilogue pays one
 # v_accvgpr_read per accumulator (bitwise the same pyramid)
