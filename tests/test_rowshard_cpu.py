@@ -1,6 +1,6 @@
 """CPU (gloo) tests of the query-row sharding collectives: partitioning and the fixed-chunk
 all-gather of ragged row slabs (RowExchange) through its persistent buffers, checked against a
-test-side restatement of the HIP reassembly.  world_size 2 and 3 processes on 127.0.0.1."""
+test-side restatement of the HIP reassembly.  world_size 2, 3 and 8 (the C5 node split) processes on 127.0.0.1."""
 import os
 import socket
 
@@ -54,7 +54,7 @@ def _worker(rank, world, port, H, W, q):
         q.put((rank, repr(e), None))
 
 
-@pytest.mark.parametrize("world,H", [(2, 60), (3, 92), (2, 7)])
+@pytest.mark.parametrize("world,H", [(2, 60), (3, 92), (2, 7), (8, 92)])   # 8: the C5 split over a node
 def test_row_exchange_chunks_reassemble(world, H):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
