@@ -316,6 +316,9 @@ PATCHES["cv_nolds"] = [("conv.hip", """            ah[i] = *reinterpret_cast<con
                 al[s] = *reinterpret_cast<const halfx8*>(wb + ((4 * oh + i + 2) * 2 + 1) * 1024);""",
                         """                ah[s] = bl * (_Float16)(i + 3);
                 al[s] = bh * (_Float16)(i + 4);""")]
+# round 6: the split's lo half as one fused op, f16(fma(hi, -1, x)) -- v_fma_mix (hi extended from f16
+# in the fma, one rounding to f16: bitwise (_Float16)(x - (float)hi), x - hi being exact)
+PATCHES["cv_fmix"] = [("conv.hip", """        lo[j] = (_Float16)(x - (float)h);""", """        lo[j] = (_Float16)__builtin_fmaf((float)h, -1.0f, x);""")]
 # round 6: the accumulators in AGPRs ("+a"): the partner block's epilogue VALU then shares no
 # register-file traffic with the MFMAs' accumulator reads / writes; the epilogue pays one
 # v_accvgpr_read per accumulator (bitwise the same pyramid)
