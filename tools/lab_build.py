@@ -319,6 +319,33 @@ PATCHES["cv_nolds"] = [("conv.hip", """            ah[i] = *reinterpret_cast<con
 # round 6: the split's lo half as one fused op, f16(fma(hi, -1, x)) -- v_fma_mix (hi extended from f16
 # in the fma, one rounding to f16: bitwise (_Float16)(x - (float)hi), x - hi being exact)
 PATCHES["cv_fmix"] = [("conv.hip", """        lo[j] = (_Float16)(x - (float)h);""", """        lo[j] = (_Float16)__builtin_fmaf((float)h, -1.0f, x);""")]
+# round 6: the split with v_fma_mixlo/hi_f16 (inline asm; the compiler turns fma(hi, -1, x) back into
+# sub + converts): lo pair = f16(x0 - hi0), f16(x1 - hi1) from the packed hi register, 2 ops per pair
+PATCHES["cv_mixasm"] = [("conv.hip", """__device__ __forceinline__ void split8(const float (&v)[8], float s, halfx8& hi, halfx8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = v[j] * s;
+        const _Float16 h = (_Float16)x;
+        hi[j] = h;
+        lo[j] = (_Float16)(x - (float)h);
+    }
+}""", """__device__ __forceinline__ void split8(const float (&v)[8], float s, halfx8& hi, halfx8& lo) {
+    typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        const float x0 = v[j] * s, x1 = v[j + 1] * s;
+        const half2v h = {(_Float16)x0, (_Float16)x1};
+        const unsigned hp = __builtin_bit_cast(unsigned, h);
+        unsigned lp;
+        asm volatile("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lp) : "v"(hp), "v"(x0));
+        asm volatile("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lp) : "v"(hp), "v"(x1));
+        const half2v l = __builtin_bit_cast(half2v, lp);
+        hi[j] = h[0];
+        hi[j + 1] = h[1];
+        lo[j] = l[0];
+        lo[j + 1] = l[1];
+    }
+}""")]
 # round 6: the accumulators in AGPRs ("+a"): the partner block's epilogue VALU then shares no
 # register-file traffic with the MFMAs' accumulator reads / writes; the epilogue pays one
 # v_accvgpr_read per accumulator (bitwise the same pyramid)
