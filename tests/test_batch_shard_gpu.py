@@ -67,3 +67,23 @@ def test_two_rank_batch_shard(launcher):
     elapsed = res["ms_per_step"] * steps / 1e3
     assert res["value"] == pytest.approx(2 * B * steps / elapsed, rel=1e-3)
     assert res["kernels"]["build"]["ms_per_launch"] > 0 and res["kernels"]["lookup"]["ms_per_launch"] > 0
+
+
+def test_two_rank_rowshard_bench():
+    """BASELINE configs[4] through bench.py itself: `bench.py --mode rowshard --gpus 2` with no launcher
+    starts 2 ranks (both on cuda:0 over gloo here), shards the 92 query rows 46 / 46, and checks one
+    sharded lookup against the unsharded CorrBlock after the timed region (bit-exact)."""
+    _gpu_untouched()
+    env = dict(os.environ, BENCH_SINGLE_DEVICE="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--mode", "rowshard", "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--no-next", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["scaling"] == "strong"
+    assert res["config"]["row_partition"] == [46, 46]
+    assert res["config"]["check_vs_unsharded"] == "bit-exact"
