@@ -272,10 +272,22 @@ struct NormState {
 };
 
 // One block: thread t folds partials t, t + NTV, ... in order, then the fixed tree.
-__global__ __launch_bounds__(NTV) void norm_finalize(const double* part, int nparts, NormState* st) {
-    __shared__ double sh[3 * NTV];
+// The moments of nparts partials (fixed order) -> the normalization state; block-wide, NTV threads.
+// Thread i combines partials i, i + NTV, ... in order, 8 loads in flight per batch.
+__device__ __forceinline__ void finalize_moments(const double* part, int nparts, double* sh, NormState* st) {
     Moments m{0.0, 0.0, 0.0};
-    for (int i = threadIdx.x; i < nparts; i += NTV) m = combine(m, {part[3 * i], part[3 * i + 1], part[3 * i + 2]});
+    for (int i0 = threadIdx.x; i0 < nparts; i0 += 8 * NTV) {
+        double v[8][3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = i0 + j * NTV;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) v[j][c] = i < nparts ? part[3 * i + c] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (i0 + j * NTV < nparts) m = combine(m, {v[j][0], v[j][1], v[j][2]});
+    }
     m = block_moments(m, sh);
     if (threadIdx.x == 0) {
         st->any = m.n > 0.0;
@@ -283,6 +295,11 @@ __global__ __launch_bounds__(NTV) void norm_finalize(const double* part, int npa
         // unbiased std; one nonzero cell gives NaN like torch.std, and then v - mean
         st->stdv = m.n > 1.0 ? (float)sqrt(m.m2 / (m.n - 1.0)) : __int_as_float(0x7fc00000);
     }
+}
+
+__global__ __launch_bounds__(NTV) void norm_finalize(const double* part, int nparts, NormState* st) {
+    __shared__ double sh[3 * NTV];
+    finalize_moments(part, nparts, sh, st);
 }
 
 __global__ __launch_bounds__(NTV) void norm_apply(float* __restrict__ g, int64_t n, const NormState* st) {
@@ -390,6 +407,319 @@ __global__ __launch_bounds__(NTV) void scan_apply(const uint32_t* __restrict__ i
 
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + NTV - 1) / NTV); }
 
+// ============================================================================================
+// DSEC, tiled (round 6).  The key-range pipeline above spends most of its time on the key range
+// itself (a 4.9 M-entry count array zeroed, scanned and indexed per cell) and on random global
+// atomics.  Here the events are bucketed by cell tile: tile (ty, tx) covers grid cells
+// [4 ty, 4 ty + 4) x [16 tx, 16 tx + 16), and its window -- the base cells its cells read, all time
+// bins -- is extended base cells [4 ty, 4 ty + 4] x [16 tx, 16 tx + 16] (the +1 halo: the first row
+// and column of the next tiles).  An event lands in every window holding its base cell (1 to 4 of
+// them, 1.33 on average), so a tile's bucket is exactly its window, contiguous in HBM; one
+// 256-thread workgroup per tile sorts it in LDS into runs (time bin, base cell), each run by event
+// index, and folds its 64 cells from there, 4 time bins at a time:
+//   vb_count    per block of VB_EPB events: the prep arithmetic, the windows, a slot within
+//               (window, block) per copy from an LDS atomic, the block's counts -> M[block][window];
+//   vb_colscan  per window, its counts over the blocks -> prefixes (in place) and its total;
+//   (scan)      exclusive scan of the totals -> window starts S;
+//   vb_scatter  each copy's (x, y, t_norm, value) and event index to S[w] + M[blk][w] + slot;
+//   vb_gather   per tile: runs counted (LDS atomics), scanned, placed, ranked by event index; then
+//               each cell folded in pass order -- the reference's serial fold, bit for bit.  A window
+//               holding more than VB_CAP events (a hot pixel, a dense stream) is read where it lies
+//               in HBM, its run order kept in a global arena (the run table stays in LDS).
+// ============================================================================================
+constexpr int VB_TY = 4, VB_TX = 16;              // cell tile
+constexpr int VB_NT = 256;                        // gather threads: 4 waves x 64 cells
+constexpr int VB_NW = VB_NT / (VB_TY * VB_TX);    // time-bin groups of the fold
+constexpr int VB_WX = VB_TX + 1, VB_WK = (VB_TY + 1) * VB_WX;   // base cells of a window, per bin
+constexpr int VB_CAP = 512;                       // window events in LDS
+constexpr int VB_MAXRUN = 2048;                   // (C + 1) * VB_WK runs per window (C <= 23)
+constexpr int VB_CNT = 1024, VB_EPB = 8 * VB_CNT; // count blocks: threads, events per block
+constexpr int VB_MAXNB = 12288;                   // windows (LDS counts of vb_count)
+static_assert(VB_NT == NTV && VB_NW * VB_TY * VB_TX == VB_NT, "vb_gather: 4 waves of one tile each");
+static_assert(VB_CAP == 2 * VB_NT, "vb_gather: two rounds of the in-place reorder");
+
+struct VTileArgs {
+    const float *p, *t, *x, *y;
+    int64_t n;
+    int C, H, W;
+    int gy, gx, nb, nblk;   // tile grid, windows (gy * gx), count blocks
+    uint32_t* cell;    // per event: extended base cell (ey << 16 | ex), or ~0u (no window)
+    uint4* slot;       // per event: slots of its copies (own, left, up, up-left)
+    float *fa, *fb;    // per event: t_norm, value
+    uint32_t* M;       // [nblk][nb]: counts, then their prefixes over the blocks
+    uint32_t* tot;     // [nb + 1]: window totals (tot[nb] = 0)
+    uint32_t* S;       // [nb + 1]: window starts
+    float4* pay;       // windowed copies (x, y, t_norm, value): at most 4n
+    int* pidx;         // windowed event index
+    double* part;
+    float* voxel;
+    uint32_t *aord, *aords;   // run order of windows past VB_CAP, at their copies' positions
+    NormState* norm;
+};
+
+// The windows of extended base cell (ey, ex): copy q = (dy, dx) bits, dy/dx = take the tile above /
+// left too (the cell is that tile's halo row / column).  -1 where the copy does not exist.
+__device__ __forceinline__ int vt_window(const VTileArgs& A, int ey, int ex, int q) {
+    const int dy = q >> 1, dx = q & 1;
+    if ((dy && (ey % VB_TY != 0)) || (dx && (ex % VB_TX != 0))) return -1;
+    const int ty = ey / VB_TY - dy, tx = ex / VB_TX - dx;
+    return (ty >= 0 && ty < A.gy && tx >= 0 && tx < A.gx) ? ty * A.gx + tx : -1;
+}
+
+__global__ __launch_bounds__(VB_CNT) void vb_count(VTileArgs A) {
+    __shared__ uint32_t hist[VB_MAXNB];
+    const int tid = threadIdx.x, blk = blockIdx.x;
+    for (int i = tid; i < A.nb; i += VB_CNT) hist[i] = 0;
+    __syncthreads();
+    const float t0 = A.t[0], dt = __fsub_rn(A.t[A.n - 1], t0);
+#pragma unroll 2
+    for (int k = 0; k < VB_EPB / VB_CNT; ++k) {
+        const int64_t e = (int64_t)blk * VB_EPB + k * VB_CNT + tid;
+        if (e >= A.n) break;
+        // dsec_utils.py:35-41 as prep_dsec
+        const float tn = __fdiv_rn(__fmul_rn((float)(A.C - 1), __fsub_rn(A.t[e], t0)), dt);
+        const int x0 = x86_i32(A.x[e]), y0 = x86_i32(A.y[e]), ti = x86_i32(tn);
+        A.fa[e] = tn;
+        A.fb[e] = __fsub_rn(__fmul_rn(2.0f, A.p[e]), 1.0f);
+        uint32_t cell = ~0u;
+        if (x0 >= -1 && x0 < A.W && y0 >= -1 && y0 < A.H && ti >= -1 && ti < A.C) {
+            const int ey = y0 + 1, ex = x0 + 1;
+            cell = (uint32_t)ey << 16 | (uint32_t)ex;
+            uint32_t s[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int w = vt_window(A, ey, ex, q);
+                s[q] = w >= 0 ? atomicAdd(&hist[w], 1u) : 0u;
+            }
+            A.slot[e] = make_uint4(s[0], s[1], s[2], s[3]);
+        }
+        A.cell[e] = cell;
+    }
+    __syncthreads();
+    uint32_t* row = A.M + (int64_t)blk * A.nb;
+    for (int i = tid; i < A.nb; i += VB_CNT) row[i] = hist[i];
+}
+
+// per window: its counts over the blocks -> exclusive prefixes (16 loads in flight per batch) and
+// its total (a last-block scan of the totals fused in here was slower: 20 vs 8 + 3 x 5 us)
+__global__ __launch_bounds__(NTV) void vb_colscan(VTileArgs A) {
+    const int b = blockIdx.x * NTV + threadIdx.x;
+    if (b > A.nb) return;
+    if (b == A.nb) { A.tot[b] = 0; return; }
+    uint32_t* __restrict__ col = A.M + b;
+    uint32_t run = 0;
+    for (int k0 = 0; k0 < A.nblk; k0 += 16) {
+        uint32_t c[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) c[j] = k0 + j < A.nblk ? col[(int64_t)(k0 + j) * A.nb] : 0u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (k0 + j < A.nblk) col[(int64_t)(k0 + j) * A.nb] = run;
+            run += c[j];
+        }
+    }
+    A.tot[b] = run;
+}
+
+__global__ __launch_bounds__(NTV) void vb_scatter(VTileArgs A) {
+    const int64_t e = blockIdx.x * (int64_t)NTV + threadIdx.x;
+    if (e >= A.n) return;
+    const uint32_t cell = A.cell[e];
+    if (cell == ~0u) return;
+    const int ey = (int)(cell >> 16), ex = (int)(cell & 0xffff);
+    const uint4 s = A.slot[e];
+    const uint32_t sl[4] = {s.x, s.y, s.z, s.w};
+    const float4 v = make_float4(A.x[e], A.y[e], A.fa[e], A.fb[e]);
+    const uint32_t* Mrow = A.M + (e / VB_EPB) * A.nb;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int w = vt_window(A, ey, ex, q);
+        if (w < 0) continue;
+        const uint32_t i = A.S[w] + Mrow[w] + sl[q];
+        A.pay[i] = v;
+        A.pidx[i] = (int)e;
+    }
+}
+
+struct VWin {
+    float4 ev[VB_CAP];             // the window's copies (8 KB; the moments' scratch at the end)
+    int idx[VB_CAP];
+    unsigned short ord[VB_CAP];    // placement order (per run, arbitrary within it)
+    unsigned short ords[VB_CAP];   // per run in event-index order
+    int off[VB_MAXRUN + 1];        // run starts, then (after placement) run ends
+    int wsum[VB_NT / kWave];
+};
+static_assert(sizeof(float4) * VB_CAP >= 3 * sizeof(double) * VB_NT, "moments scratch");
+
+// :48 value * (1 - |xlim - x|) * (1 - |ylim - y|) * (1 - |tlim - t_norm|), left to right
+__device__ __forceinline__ float vt_term(float4 ev, float fx, float fy, float ft) {
+    float wgt = __fmul_rn(ev.w, __fsub_rn(1.0f, fabsf(__fsub_rn(fx, ev.x))));
+    wgt = __fmul_rn(wgt, __fsub_rn(1.0f, fabsf(__fsub_rn(fy, ev.y))));
+    return __fmul_rn(wgt, __fsub_rn(1.0f, fabsf(__fsub_rn(ft, ev.z))));
+}
+
+__global__ __launch_bounds__(VB_NT) void vb_gather(VTileArgs A, int normalize) {
+    __shared__ VWin L;
+    const int tid = threadIdx.x, lane = tid % kWave, wv = tid / kWave;
+    const int tile = blockIdx.x, cy = tile / A.gx, cx = tile % A.gx;
+    const int ey0 = cy * VB_TY, ex0 = cx * VB_TX;   // window origin on the extended base-cell grid
+    const int nrun = (A.C + 1) * VB_WK;
+    const uint32_t s0 = A.S[tile];
+    const int n = (int)(A.S[tile + 1] - s0);
+    const bool ar = n > VB_CAP;   // uniform: the window is read where it lies
+    const float4* gev = A.pay + s0;
+    const int* gidx = A.pidx + s0;
+    uint32_t* aord = A.aord + s0;
+    uint32_t* aords = A.aords + s0;
+    // run of a copy: (bin ti + 1, window row, window column)
+    auto run_of = [&](const float4& ev) {
+        return ((x86_i32(ev.z) + 1) * (VB_TY + 1) + x86_i32(ev.y) + 1 - ey0) * VB_WX + x86_i32(ev.x) + 1 - ex0;
+    };
+    for (int k = tid; k <= nrun; k += VB_NT) L.off[k] = 0;
+    __syncthreads();
+    for (int j = tid; j < n; j += VB_NT) {   // count
+        const float4 ev = gev[j];
+        if (!ar) {
+            L.ev[j] = ev;
+            L.idx[j] = gidx[j];
+        }
+        atomicAdd(&L.off[run_of(ev)], 1);
+    }
+    __syncthreads();
+    {   // exclusive scan of the nrun counts: per thread a contiguous chunk, waves, then the block
+        constexpr int PER = (VB_MAXRUN + VB_NT - 1) / VB_NT;
+        const int k0 = tid * PER;
+        int v[PER], s = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            v[i] = k0 + i < nrun ? L.off[k0 + i] : 0;
+            s += v[i];
+        }
+        int inc = s;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int u = __shfl_up(inc, d, kWave);
+            if (lane >= d) inc += u;
+        }
+        if (lane == kWave - 1) L.wsum[wv] = inc;
+        __syncthreads();
+        int base = inc - s;
+        for (int w = 0; w < wv; ++w) base += L.wsum[w];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            if (k0 + i < nrun) L.off[k0 + i] = base;
+            base += v[i];
+        }
+    }
+    __syncthreads();
+    for (int j = tid; j < n; j += VB_NT) {   // place: off[r] walks from its run's start to its end
+        const int r = run_of(ar ? gev[j] : L.ev[j]);
+        const int pos = atomicAdd(&L.off[r], 1);
+        if (ar) aord[pos] = (uint32_t)j;
+        else L.ord[pos] = (unsigned short)j;
+    }
+    __syncthreads();
+    for (int j = tid; j < n; j += VB_NT) {   // rank within the run by event index
+        const int r = run_of(ar ? gev[j] : L.ev[j]);
+        const int lo = r > 0 ? L.off[r - 1] : 0, hi = L.off[r];
+        int rk = 0;
+        if (ar) {
+            const int me = gidx[j];
+            for (int i = lo; i < hi; ++i) rk += gidx[aord[i]] < me;
+            aords[lo + rk] = (uint32_t)j;
+        } else {
+            const int me = L.idx[j];
+            for (int i = lo; i < hi; ++i) rk += L.idx[L.ord[i]] < me;
+            L.ords[lo + rk] = (unsigned short)j;
+        }
+    }
+    __syncthreads();
+
+    if (!ar) {   // the window's events into run order in place: the fold reads L.ev[i] directly
+        const int j0 = tid, j1 = tid + VB_NT;   // VB_CAP = 2 VB_NT
+        const float4 e0 = L.ev[j0 < n ? L.ords[j0] : 0], e1 = L.ev[j1 < n ? L.ords[j1] : 0];
+        __syncthreads();
+        if (j0 < n) L.ev[j0] = e0;
+        if (j1 < n) L.ev[j1] = e1;
+        __syncthreads();
+    }
+
+    // wave wv folds time bins [tc0, tc1) of its lane's cell
+    const int ly = lane / VB_TX, lx = lane % VB_TX;
+    const int yc = ey0 + ly, xc = ex0 + lx;
+    const int nper = (A.C + VB_NW - 1) / VB_NW, tc0 = wv * nper, tc1 = min(A.C, tc0 + nper);
+    double cn = 0.0, cs = 0.0, css = 0.0;
+    if (yc < A.H && xc < A.W && tc0 < tc1) {
+        const float fx = (float)xc, fy = (float)yc;
+        // run bounds of bin e around this cell: row ly + 1 (u) and row ly (d), columns lx and lx + 1:
+        // column lx = [x0, x1), column lx + 1 = [x1, x2)
+        struct Bounds { int u0, u1, u2, d0, d1, d2; };
+        auto bounds = [&](int e) {
+            const int ru = (e * (VB_TY + 1) + ly + 1) * VB_WX + lx, rd = ru - VB_WX;
+            return Bounds{L.off[ru - 1], L.off[ru], L.off[ru + 1], rd > 0 ? L.off[rd - 1] : 0, L.off[rd], L.off[rd + 1]};
+        };
+        Bounds bp = bounds(tc0);
+        for (int tc = tc0; tc < tc1; ++tc) {
+            const Bounds bn = bounds(tc + 1);
+            const float ft = (float)tc;
+            // dsec_utils.py:43-45 pass order: xlim outer, ylim, tlim inner; pass (a, b, c) reads base
+            // cell (tc - c, yc - b, xc - a) = run (bin tc + 1 - c, row ly + 1 - b, column lx + 1 - a)
+            const int lo[8] = {bn.u1, bp.u1, bn.d1, bp.d1, bn.u0, bp.u0, bn.d0, bp.d0};
+            const int hi[8] = {bn.u2, bp.u2, bn.d2, bp.d2, bn.u1, bp.u1, bn.d1, bp.d1};
+            // the 8 runs as one sequence: k -> i = k + dl[p] for the pass p with end[p - 1] <= k < end[p]
+            int end[8], dl[8], tot = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                dl[q] = lo[q] - tot;
+                tot += hi[q] - lo[q];
+                end[q] = tot;
+            }
+            float acc = 0.0f;
+            for (int k = 0; k < tot; ++k) {
+                int i = k + dl[7];
+#pragma unroll
+                for (int q = 6; q >= 0; --q) i = k < end[q] ? k + dl[q] : i;
+                acc = __fadd_rn(acc, vt_term(ar ? gev[aords[i]] : L.ev[i], fx, fy, ft));
+            }
+            A.voxel[((int64_t)tc * A.H + yc) * A.W + xc] = acc;
+            if (normalize && acc != 0.0f) {
+                const double v = (double)acc;
+                cn += 1.0;
+                cs += v;
+                css = fma(v, v, css);
+            }
+            bp = bn;
+        }
+    }
+    if (normalize) {   // (count, mean, M2) of this thread's nonzero cells, then a fixed-order tree
+        Moments m{0.0, 0.0, 0.0};
+        if (cn > 0.0) {
+            const double mean = cs / cn;
+            m = {cn, mean, fmax(css - cs * mean, 0.0)};
+        }
+        __syncthreads();   // the fold's reads of L.ev are done: its bytes become the scratch
+        m = block_moments(m, reinterpret_cast<double*>(L.ev));
+        if (tid == 0) {
+            A.part[3 * tile] = m.n;
+            A.part[3 * tile + 1] = m.mean;
+            A.part[3 * tile + 2] = m.m2;
+        }
+    }
+}
+
+// The tiled DSEC path's tile grid, or false where it does not apply (its LDS counts or run table
+// would overflow, or 32-bit copy positions): then the key-range pipeline runs.
+struct VTileGeom { int gy, gx, nb, nblk; };
+inline bool vtile_geom(int64_t n, int C, int H, int W, VTileGeom* g) {
+    g->gy = (H + VB_TY - 1) / VB_TY;
+    g->gx = (W + VB_TX - 1) / VB_TX;
+    const int64_t nb = (int64_t)g->gy * g->gx;
+    g->nb = (int)std::min<int64_t>(nb, 1 << 30);
+    g->nblk = (int)((n + VB_EPB - 1) / VB_EPB);
+    return nb <= VB_MAXNB && (int64_t)(C + 1) * VB_WK <= VB_MAXRUN && 4 * n < (int64_t)1 << 31 && W < 65535 &&
+           H < 65535;
+}
+
 inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // Workspace carve-up (every piece 256-byte aligned).
@@ -425,6 +755,76 @@ inline int hip_status() {
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
 }
 
+// Workspace of the tiled DSEC path.
+struct VTileWs {
+    size_t cell, slot, fa, fb, M, tot, S, sums, pay, pidx, norm, part, aord, aords, total;
+};
+
+void plan_tiled(int64_t n, const VTileGeom& g, VTileWs* w) {
+    size_t o = 0;
+    auto take = [&](size_t bytes) { const size_t at = o; o += align256(bytes); return at; };
+    const size_t copies = 4 * (size_t)n;   // an event lies in at most 4 windows
+    w->cell = take(4 * (size_t)n);
+    w->slot = take(16 * (size_t)n);
+    w->fa = take(4 * (size_t)n);
+    w->fb = take(4 * (size_t)n);
+    w->M = take(4 * (size_t)g.nblk * g.nb);
+    w->tot = take(4 * ((size_t)g.nb + 1));
+    w->S = take(4 * ((size_t)g.nb + 1));
+    w->sums = take(4 * (((size_t)g.nb + 1 + SCAN_T - 1) / SCAN_T));
+    w->pay = take(16 * copies);
+    w->pidx = take(4 * copies);
+    w->norm = take(sizeof(NormState));
+    w->part = take(3 * 8 * (size_t)g.nb);
+    w->aord = take(4 * copies);
+    w->aords = take(4 * copies);
+    w->total = o;
+}
+
+int launch_voxel_tiled(const float* p, const float* t, const float* x, const float* y, int64_t n, int C, int H,
+                       int W, int normalize, float* voxel, void* workspace, const VTileGeom& g, hipStream_t stream) {
+    VTileWs w;
+    plan_tiled(n, g, &w);
+    char* base = (char*)workspace;
+    VTileArgs A{};
+    A.p = p; A.t = t; A.x = x; A.y = y;
+    A.n = n; A.C = C; A.H = H; A.W = W;
+    A.gy = g.gy; A.gx = g.gx; A.nb = g.nb; A.nblk = g.nblk;
+    A.cell = (uint32_t*)(base + w.cell);
+    A.slot = (uint4*)(base + w.slot);
+    A.fa = (float*)(base + w.fa);
+    A.fb = (float*)(base + w.fb);
+    A.M = (uint32_t*)(base + w.M);
+    A.tot = (uint32_t*)(base + w.tot);
+    A.S = (uint32_t*)(base + w.S);
+    A.pay = (float4*)(base + w.pay);
+    A.pidx = (int*)(base + w.pidx);
+    A.part = (double*)(base + w.part);
+    A.voxel = voxel;
+    A.aord = (uint32_t*)(base + w.aord);
+    A.aords = (uint32_t*)(base + w.aords);
+    A.norm = (NormState*)(base + w.norm);
+    int st;
+    hipLaunchKernelGGL(vb_count, dim3(g.nblk), dim3(VB_CNT), 0, stream, A);
+    hipLaunchKernelGGL(vb_colscan, dim3((unsigned)((g.nb + 1 + NTV - 1) / NTV)), dim3(NTV), 0, stream, A);
+    {   // window starts: exclusive scan of the nb + 1 totals (tot[nb] = 0: S[nb] = every copy)
+        const int64_t K1 = (int64_t)g.nb + 1;
+        const unsigned nbk = (unsigned)((K1 + SCAN_T - 1) / SCAN_T);
+        uint32_t* sums = (uint32_t*)(base + w.sums);
+        hipLaunchKernelGGL(scan_reduce, dim3(nbk), dim3(NTV), 0, stream, A.tot, K1, sums);
+        hipLaunchKernelGGL(scan_sums, dim3(1), dim3(NTV), 0, stream, sums, (int)nbk);
+        hipLaunchKernelGGL(scan_apply, dim3(nbk), dim3(NTV), 0, stream, A.tot, K1, sums, A.S);
+    }
+    hipLaunchKernelGGL(vb_scatter, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
+    hipLaunchKernelGGL(vb_gather, dim3(g.nb), dim3(VB_NT), 0, stream, A, normalize);
+    if ((st = hip_status()) != ECORR_OK) return st;
+    if (normalize) {
+        hipLaunchKernelGGL(norm_finalize, dim3(1), dim3(NTV), 0, stream, A.part, g.nb, A.norm);
+        hipLaunchKernelGGL(norm_apply, dim3(kRedBlocks), dim3(NTV), 0, stream, voxel, (int64_t)C * H * W, A.norm);
+    }
+    return hip_status();
+}
+
 }  // namespace
 
 uint32_t voxel_key_range(bool dsec, int C, int H, int W) {
@@ -432,6 +832,13 @@ uint32_t voxel_key_range(bool dsec, int C, int H, int W) {
 }
 
 int voxel_workspace_bytes(bool dsec, int64_t n, int C, int H, int W, int64_t* bytes) {
+    VTileGeom g;
+    if (dsec && vtile_geom(n, C, H, W, &g)) {
+        VTileWs tw;
+        plan_tiled(n, g, &tw);
+        *bytes = (int64_t)tw.total;
+        return ECORR_OK;
+    }
     VoxelWs w;
     const int st = plan(n, voxel_key_range(dsec, C, H, W), (int64_t)C * H * W, &w);
     if (st == ECORR_OK) *bytes = (int64_t)w.total;
@@ -441,6 +848,9 @@ int voxel_workspace_bytes(bool dsec, int64_t n, int C, int H, int W, int64_t* by
 int launch_voxel(bool dsec, const float* p, const float* t, const float* x, const float* y, const double* ev,
                  int64_t n, int C, int H, int W, int normalize, float* voxel, int* bad, void* workspace,
                  hipStream_t stream) {
+    VTileGeom g;
+    if (dsec && vtile_geom(n, C, H, W, &g))
+        return launch_voxel_tiled(p, t, x, y, n, C, H, W, normalize, voxel, workspace, g, stream);
     VoxelArgs A{};
     A.p = p; A.t = t; A.x = x; A.y = y; A.ev = ev;
     A.n = n; A.C = C; A.H = H; A.W = W;

@@ -85,6 +85,37 @@ def test_voxel_mvsec_full_res_vs_oracle(ea):
     assert not bad and oracle.same_bits(g, ref)
 
 
+@pytest.mark.parametrize("case", ["hot_pixel", "dense_ragged", "sparse_ragged", "unsorted_t"])
+def test_voxel_dsec_tiled_paths_vs_oracle(ea, case):
+    """The tiled DSEC path (round 6): 8 x 64 cell tiles walking the time bins, each bin's window in
+    LDS -- or, past VB_CAP = 1024 events of one bin's window, in the global arena.  hot_pixel: 60% of
+    the events on one base cell (~3,000 per bin in one window: the arena, runs of thousands ranked
+    by event index); dense_ragged: every window past the cap, tiles cut by H % 8 and W % 64;
+    sparse_ragged: the LDS path on partial tiles; unsorted_t: timestamps not in order (the bucket
+    lists then interleave bins' events arbitrarily).  Accumulated grid bit-exact with the serial
+    fold, normalized within NORM_TOL."""
+    if case == "hot_pixel":
+        n, C, H, W = 20_000, 3, 16, 64
+        p, t, x, y = prng.dsec_events(730, n, H, W)
+        hot = prng.uniform(731, (n,)) < 0.6
+        x[hot] = np.float32(10.3)
+        y[hot] = np.float32(5.7)
+    elif case == "dense_ragged":
+        n, C, H, W = 60_000, 4, 21, 130
+        p, t, x, y = prng.dsec_events(740, n, H, W)
+    elif case == "sparse_ragged":
+        n, C, H, W = 3_000, 5, 21, 70
+        p, t, x, y = prng.dsec_events(750, n, H, W)
+    else:
+        n, C, H, W = 8_000, 4, 30, 90
+        p, t, x, y = prng.dsec_events(760, n, H, W)
+        t = t[np.argsort(prng.uniform(761, (n,)))].copy()   # a permutation: t[0], t[-1] arbitrary
+    g = _dsec(ea, p, t, x, y, C, H, W, False)
+    assert oracle.same_bits(g, oracle.voxel_dsec(p, t, x, y, C, H, W, False)), case
+    np.testing.assert_allclose(_dsec(ea, p, t, x, y, C, H, W, True), oracle.voxel_dsec(p, t, x, y, C, H, W, True),
+                               rtol=NORM_TOL, atol=NORM_TOL, err_msg=case)
+
+
 def test_voxel_rejects_cpu_events(ea):
     p, t, x, y = prng.dsec_events(720, 10, 4, 4)
     with pytest.raises(RuntimeError):
