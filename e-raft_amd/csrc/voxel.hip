@@ -438,6 +438,12 @@ constexpr int VB_MAXNB = 12288;                   // windows (LDS counts of vb_c
 static_assert(VB_NT == NTV && VB_NW * VB_TY * VB_TX == VB_NT, "vb_gather: 4 waves of one tile each");
 static_assert(VB_CAP == 2 * VB_NT, "vb_gather: two rounds of the in-place reorder");
 
+// a window's copy of an event: (x, y, t_norm, value) and the event index, one 32-byte sector
+struct alignas(32) VCopy {
+    float4 ev;
+    int idx, pad[3];
+};
+
 struct VTileArgs {
     const float *p, *t, *x, *y;
     int64_t n;
@@ -449,8 +455,7 @@ struct VTileArgs {
     uint32_t* M;       // [nblk][nb]: counts, then their prefixes over the blocks
     uint32_t* tot;     // [nb + 1]: window totals (tot[nb] = 0)
     uint32_t* S;       // [nb + 1]: window starts
-    float4* pay;       // windowed copies (x, y, t_norm, value): at most 4n
-    int* pidx;         // windowed event index
+    VCopy* pay;        // windowed copies: at most 4n
     double* part;
     float* voxel;
     uint32_t *aord, *aords;   // run order of windows past VB_CAP, at their copies' positions
@@ -536,8 +541,8 @@ __global__ __launch_bounds__(NTV) void vb_scatter(VTileArgs A) {
         const int w = vt_window(A, ey, ex, q);
         if (w < 0) continue;
         const uint32_t i = A.S[w] + Mrow[w] + sl[q];
-        A.pay[i] = v;
-        A.pidx[i] = (int)e;
+        A.pay[i].ev = v;
+        A.pay[i].idx = (int)e;
     }
 }
 
@@ -567,8 +572,7 @@ __global__ __launch_bounds__(VB_NT) void vb_gather(VTileArgs A, int normalize) {
     const uint32_t s0 = A.S[tile];
     const int n = (int)(A.S[tile + 1] - s0);
     const bool ar = n > VB_CAP;   // uniform: the window is read where it lies
-    const float4* gev = A.pay + s0;
-    const int* gidx = A.pidx + s0;
+    const VCopy* gc = A.pay + s0;
     uint32_t* aord = A.aord + s0;
     uint32_t* aords = A.aords + s0;
     // run of a copy: (bin ti + 1, window row, window column)
@@ -578,10 +582,10 @@ __global__ __launch_bounds__(VB_NT) void vb_gather(VTileArgs A, int normalize) {
     for (int k = tid; k <= nrun; k += VB_NT) L.off[k] = 0;
     __syncthreads();
     for (int j = tid; j < n; j += VB_NT) {   // count
-        const float4 ev = gev[j];
+        const float4 ev = gc[j].ev;
         if (!ar) {
             L.ev[j] = ev;
-            L.idx[j] = gidx[j];
+            L.idx[j] = gc[j].idx;
         }
         atomicAdd(&L.off[run_of(ev)], 1);
     }
@@ -613,19 +617,19 @@ __global__ __launch_bounds__(VB_NT) void vb_gather(VTileArgs A, int normalize) {
     }
     __syncthreads();
     for (int j = tid; j < n; j += VB_NT) {   // place: off[r] walks from its run's start to its end
-        const int r = run_of(ar ? gev[j] : L.ev[j]);
+        const int r = run_of(ar ? gc[j].ev : L.ev[j]);
         const int pos = atomicAdd(&L.off[r], 1);
         if (ar) aord[pos] = (uint32_t)j;
         else L.ord[pos] = (unsigned short)j;
     }
     __syncthreads();
     for (int j = tid; j < n; j += VB_NT) {   // rank within the run by event index
-        const int r = run_of(ar ? gev[j] : L.ev[j]);
+        const int r = run_of(ar ? gc[j].ev : L.ev[j]);
         const int lo = r > 0 ? L.off[r - 1] : 0, hi = L.off[r];
         int rk = 0;
         if (ar) {
-            const int me = gidx[j];
-            for (int i = lo; i < hi; ++i) rk += gidx[aord[i]] < me;
+            const int me = gc[j].idx;
+            for (int i = lo; i < hi; ++i) rk += gc[aord[i]].idx < me;
             aords[lo + rk] = (uint32_t)j;
         } else {
             const int me = L.idx[j];
@@ -679,7 +683,7 @@ __global__ __launch_bounds__(VB_NT) void vb_gather(VTileArgs A, int normalize) {
                 int i = k + dl[7];
 #pragma unroll
                 for (int q = 6; q >= 0; --q) i = k < end[q] ? k + dl[q] : i;
-                acc = __fadd_rn(acc, vt_term(ar ? gev[aords[i]] : L.ev[i], fx, fy, ft));
+                acc = __fadd_rn(acc, vt_term(ar ? gc[aords[i]].ev : L.ev[i], fx, fy, ft));
             }
             A.voxel[((int64_t)tc * A.H + yc) * A.W + xc] = acc;
             if (normalize && acc != 0.0f) {
@@ -757,7 +761,7 @@ inline int hip_status() {
 
 // Workspace of the tiled DSEC path.
 struct VTileWs {
-    size_t cell, slot, fa, fb, M, tot, S, sums, pay, pidx, norm, part, aord, aords, total;
+    size_t cell, slot, fa, fb, M, tot, S, sums, pay, norm, part, aord, aords, total;
 };
 
 void plan_tiled(int64_t n, const VTileGeom& g, VTileWs* w) {
@@ -772,8 +776,7 @@ void plan_tiled(int64_t n, const VTileGeom& g, VTileWs* w) {
     w->tot = take(4 * ((size_t)g.nb + 1));
     w->S = take(4 * ((size_t)g.nb + 1));
     w->sums = take(4 * (((size_t)g.nb + 1 + SCAN_T - 1) / SCAN_T));
-    w->pay = take(16 * copies);
-    w->pidx = take(4 * copies);
+    w->pay = take(sizeof(VCopy) * copies);
     w->norm = take(sizeof(NormState));
     w->part = take(3 * 8 * (size_t)g.nb);
     w->aord = take(4 * copies);
@@ -797,8 +800,7 @@ int launch_voxel_tiled(const float* p, const float* t, const float* x, const flo
     A.M = (uint32_t*)(base + w.M);
     A.tot = (uint32_t*)(base + w.tot);
     A.S = (uint32_t*)(base + w.S);
-    A.pay = (float4*)(base + w.pay);
-    A.pidx = (int*)(base + w.pidx);
+    A.pay = (VCopy*)(base + w.pay);
     A.part = (double*)(base + w.part);
     A.voxel = voxel;
     A.aord = (uint32_t*)(base + w.aord);
