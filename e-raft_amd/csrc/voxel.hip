@@ -302,13 +302,45 @@ __global__ __launch_bounds__(NTV) void norm_finalize(const double* part, int npa
     finalize_moments(part, nparts, sh, st);
 }
 
+__device__ __forceinline__ float norm_one(float v, float mean, float sd) {
+    return v != 0.0f ? (sd > 0.0f ? __fdiv_rn(__fsub_rn(v, mean), sd) : __fsub_rn(v, mean)) : v;
+}
+
+// (v - mean) / std on the nonzero cells; 16-byte accesses (the grid is 16-byte aligned: checked by
+// launch_norm_apply), the n % 4 tail by thread 0 of block 0
 __global__ __launch_bounds__(NTV) void norm_apply(float* __restrict__ g, int64_t n, const NormState* st) {
+    if (!st->any) return;
+    const float mean = st->mean, sd = st->stdv;
+    float4* g4 = reinterpret_cast<float4*>(g);
+    const int64_t n4 = n / 4;
+    for (int64_t i = blockIdx.x * (int64_t)NTV + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NTV) {
+        float4 v = g4[i];
+        if (v.x != 0.0f || v.y != 0.0f || v.z != 0.0f || v.w != 0.0f) {
+            v.x = norm_one(v.x, mean, sd);
+            v.y = norm_one(v.y, mean, sd);
+            v.z = norm_one(v.z, mean, sd);
+            v.w = norm_one(v.w, mean, sd);
+            g4[i] = v;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int64_t i = 4 * n4; i < n; ++i) g[i] = norm_one(g[i], mean, sd);
+}
+
+__global__ __launch_bounds__(NTV) void norm_apply_scalar(float* __restrict__ g, int64_t n, const NormState* st) {
     if (!st->any) return;
     const float mean = st->mean, sd = st->stdv;
     for (int64_t i = blockIdx.x * (int64_t)NTV + threadIdx.x; i < n; i += (int64_t)gridDim.x * NTV) {
         const float v = g[i];
-        if (v != 0.0f) g[i] = sd > 0.0f ? __fdiv_rn(__fsub_rn(v, mean), sd) : __fsub_rn(v, mean);
+        if (v != 0.0f) g[i] = norm_one(v, mean, sd);
     }
+}
+
+void launch_norm_apply(float* g, int64_t n, const NormState* st, hipStream_t stream) {
+    if (((uintptr_t)g & 15) == 0)
+        hipLaunchKernelGGL(norm_apply, dim3(kRedBlocks), dim3(NTV), 0, stream, g, n, st);
+    else
+        hipLaunchKernelGGL(norm_apply_scalar, dim3(kRedBlocks), dim3(NTV), 0, stream, g, n, st);
 }
 
 // Exclusive uint32 scan of the per-key counts (wrapping adds, like any uint32 scan): SCAN_T
@@ -822,7 +854,7 @@ int launch_voxel_tiled(const float* p, const float* t, const float* x, const flo
     if ((st = hip_status()) != ECORR_OK) return st;
     if (normalize) {
         hipLaunchKernelGGL(norm_finalize, dim3(1), dim3(NTV), 0, stream, A.part, g.nb, A.norm);
-        hipLaunchKernelGGL(norm_apply, dim3(kRedBlocks), dim3(NTV), 0, stream, voxel, (int64_t)C * H * W, A.norm);
+        launch_norm_apply(voxel, (int64_t)C * H * W, A.norm, stream);
     }
     return hip_status();
 }
@@ -900,7 +932,7 @@ int launch_voxel(bool dsec, const float* p, const float* t, const float* x, cons
     if ((st = hip_status()) != ECORR_OK) return st;
     if (normalize) {
         hipLaunchKernelGGL(norm_finalize, dim3(1), dim3(NTV), 0, stream, A.part, (int)gblocks, ns);
-        hipLaunchKernelGGL(norm_apply, dim3(kRedBlocks), dim3(NTV), 0, stream, voxel, cells, ns);
+        launch_norm_apply(voxel, cells, ns, stream);
     }
     return hip_status();
 }

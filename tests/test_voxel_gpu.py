@@ -87,13 +87,14 @@ def test_voxel_mvsec_full_res_vs_oracle(ea):
 
 @pytest.mark.parametrize("case", ["hot_pixel", "dense_ragged", "sparse_ragged", "unsorted_t"])
 def test_voxel_dsec_tiled_paths_vs_oracle(ea, case):
-    """The tiled DSEC path (round 6): 8 x 64 cell tiles walking the time bins, each bin's window in
-    LDS -- or, past VB_CAP = 1024 events of one bin's window, in the global arena.  hot_pixel: 60% of
-    the events on one base cell (~3,000 per bin in one window: the arena, runs of thousands ranked
-    by event index); dense_ragged: every window past the cap, tiles cut by H % 8 and W % 64;
-    sparse_ragged: the LDS path on partial tiles; unsorted_t: timestamps not in order (the bucket
-    lists then interleave bins' events arbitrarily).  Accumulated grid bit-exact with the serial
-    fold, normalized within NORM_TOL."""
+    """The tiled DSEC path (round 6): 4 x 16 cell tiles, each reading its window (its base cells and
+    the +1 halo, every time bin) from one contiguous bucket -- in LDS, or past VB_CAP = 512 events
+    where it lies in HBM with its run order in the global arena.  hot_pixel: 60% of the events on one
+    base cell (~12,000 in one window: the arena, runs of thousands ranked by event index);
+    dense_ragged: every window past the cap (~1,800 events each), tiles cut by H % 4 and W % 16;
+    sparse_ragged: the LDS path on partial tiles; unsorted_t: timestamps not in order (a bucket then
+    interleaves bins' events arbitrarily).  Accumulated grid bit-exact with the serial fold,
+    normalized within NORM_TOL."""
     if case == "hot_pixel":
         n, C, H, W = 20_000, 3, 16, 64
         p, t, x, y = prng.dsec_events(730, n, H, W)
@@ -114,6 +115,26 @@ def test_voxel_dsec_tiled_paths_vs_oracle(ea, case):
     assert oracle.same_bits(g, oracle.voxel_dsec(p, t, x, y, C, H, W, False)), case
     np.testing.assert_allclose(_dsec(ea, p, t, x, y, C, H, W, True), oracle.voxel_dsec(p, t, x, y, C, H, W, True),
                                rtol=NORM_TOL, atol=NORM_TOL, err_msg=case)
+
+
+def test_voxel_normalize_unaligned_output(ea):
+    """norm_apply's 16-byte path needs a 16-byte-aligned grid: an output 4 bytes into a buffer takes
+    the scalar kernel, and C * H * W = 105 (n % 4 = 1) exercises the vector path's tail; both equal
+    the aligned run bit for bit."""
+    import ctypes
+    from eraft_amd import _lib, voxel
+    n, C, H, W = 2_000, 3, 5, 7
+    p, t, x, y = (torch.from_numpy(v).cuda() for v in prng.dsec_events(770, n, H, W))
+    ref = ea.VoxelGrid((C, H, W), normalize=True).convert({"p": p, "t": t, "x": x, "y": y})
+    buf = torch.full((C * H * W + 1,), float("nan"), device="cuda")
+    out = buf[1:]
+    assert out.data_ptr() % 16 == 4
+    ws = voxel._workspace(True, n, C, H, W, p.device)
+    _lib.check(_lib.lib().ecorr_voxel_grid_dsec(p.data_ptr(), t.data_ptr(), x.data_ptr(), y.data_ptr(), n, C, H, W,
+                                                1, out.data_ptr(), ws.data_ptr(), _lib.stream_of(p)), "voxel")
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(C, H, W), ref)
+    assert (ref != 0).any()
 
 
 def test_voxel_rejects_cpu_events(ea):
