@@ -452,7 +452,7 @@ inline unsigned blocks_for(int64_t n) { return (unsigned)((n + NTV - 1) / NTV); 
 //   vb_count    per block of VB_EPB events: the prep arithmetic, the windows, a slot within
 //               (window, block) per copy from an LDS atomic, the block's counts -> M[block][window];
 //   vb_colscan  per window, its counts over the blocks -> prefixes (in place) and its total;
-//   (scan)      exclusive scan of the totals -> window starts S;
+//   vb_starts   one block: exclusive scan of the totals -> window starts S;
 //   vb_scatter  each copy's (x, y, t_norm, value) and event index to S[w] + M[blk][w] + slot;
 //   vb_gather   per tile: runs counted (LDS atomics), scanned, placed, ranked by event index; then
 //               each cell folded in pass order -- the reference's serial fold, bit for bit.  A window
@@ -556,6 +556,27 @@ __global__ __launch_bounds__(NTV) void vb_colscan(VTileArgs A) {
         }
     }
     A.tot[b] = run;
+}
+
+// window starts: exclusive scan of the nb + 1 totals (tot[nb] = 0); one block, each thread a
+// contiguous chunk (8 loads in flight per batch)
+__global__ __launch_bounds__(NTV) void vb_starts(VTileArgs A) {
+    __shared__ uint32_t sh[NTV / kWave];
+    const int K = A.nb + 1, per = (K + NTV - 1) / NTV, k0 = threadIdx.x * per, k1 = min(K, k0 + per);
+    uint32_t s = 0;
+    for (int k = k0; k < k1; k += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = k + j < k1 ? A.tot[k + j] : 0u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(s, sh, total);
+    for (int k = k0; k < k1; ++k) {
+        A.S[k] = run;
+        run += A.tot[k];
+    }
 }
 
 __global__ __launch_bounds__(NTV) void vb_scatter(VTileArgs A) {
@@ -793,7 +814,7 @@ inline int hip_status() {
 
 // Workspace of the tiled DSEC path.
 struct VTileWs {
-    size_t cell, slot, fa, fb, M, tot, S, sums, pay, norm, part, aord, aords, total;
+    size_t cell, slot, fa, fb, M, tot, S, pay, norm, part, aord, aords, total;
 };
 
 void plan_tiled(int64_t n, const VTileGeom& g, VTileWs* w) {
@@ -807,7 +828,6 @@ void plan_tiled(int64_t n, const VTileGeom& g, VTileWs* w) {
     w->M = take(4 * (size_t)g.nblk * g.nb);
     w->tot = take(4 * ((size_t)g.nb + 1));
     w->S = take(4 * ((size_t)g.nb + 1));
-    w->sums = take(4 * (((size_t)g.nb + 1 + SCAN_T - 1) / SCAN_T));
     w->pay = take(sizeof(VCopy) * copies);
     w->norm = take(sizeof(NormState));
     w->part = take(3 * 8 * (size_t)g.nb);
@@ -841,14 +861,7 @@ int launch_voxel_tiled(const float* p, const float* t, const float* x, const flo
     int st;
     hipLaunchKernelGGL(vb_count, dim3(g.nblk), dim3(VB_CNT), 0, stream, A);
     hipLaunchKernelGGL(vb_colscan, dim3((unsigned)((g.nb + 1 + NTV - 1) / NTV)), dim3(NTV), 0, stream, A);
-    {   // window starts: exclusive scan of the nb + 1 totals (tot[nb] = 0: S[nb] = every copy)
-        const int64_t K1 = (int64_t)g.nb + 1;
-        const unsigned nbk = (unsigned)((K1 + SCAN_T - 1) / SCAN_T);
-        uint32_t* sums = (uint32_t*)(base + w.sums);
-        hipLaunchKernelGGL(scan_reduce, dim3(nbk), dim3(NTV), 0, stream, A.tot, K1, sums);
-        hipLaunchKernelGGL(scan_sums, dim3(1), dim3(NTV), 0, stream, sums, (int)nbk);
-        hipLaunchKernelGGL(scan_apply, dim3(nbk), dim3(NTV), 0, stream, A.tot, K1, sums, A.S);
-    }
+    hipLaunchKernelGGL(vb_starts, dim3(1), dim3(NTV), 0, stream, A);
     hipLaunchKernelGGL(vb_scatter, dim3(blocks_for(n)), dim3(NTV), 0, stream, A);
     hipLaunchKernelGGL(vb_gather, dim3(g.nb), dim3(VB_NT), 0, stream, A, normalize);
     if ((st = hip_status()) != ECORR_OK) return st;
