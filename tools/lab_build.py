@@ -738,14 +738,19 @@ PATCHES["cv_nowdma"] = [("conv.hip", "        issue_w(min(c + 2, nkc - 1), (c + 
 
 # recipe-name prefix -> the lab_patches diff it applies on top of
 # voxel tiled gather (timing only unless noted): phases skipped / LDS capacity
-_VX_FOLD = "    if (yc < A.H && xc < A.W) {\n        const float fx = (float)xc, fy = (float)yc;\n        for (int tc = wv;"
-PATCHES["vx_nofold_"] = [("voxel.hip", _VX_FOLD, _VX_FOLD.replace("if (yc < A.H && xc < A.W)", "if (yc < 0)"))]
+_VX_FOLD = "    if (yc < A.H && xc < A.W && tc0 < tc1) {"
+PATCHES["vx_nofold_"] = [("voxel.hip", _VX_FOLD, "    if (yc < 0) {")]
 PATCHES["vx_norank_"] = [("voxel.hip", "    for (int j = tid; j < n; j += VB_NT) {   // rank within the run by event index",
                           "    for (int j = tid; j < 0; j += VB_NT) {   // rank within the run by event index")]
 PATCHES["vx_noplace_"] = [("voxel.hip", "    for (int j = tid; j < n; j += VB_NT) {   // place: off[r] walks",
                            "    for (int j = tid; j < 0; j += VB_NT) {   // place: off[r] walks")]
 COMBOS["vx_nofold"] = ["vx_nofold_"]
-COMBOS["vx_countonly"] = ["vx_nofold_", "vx_norank_", "vx_noplace_"]
+COMBOS["vx_countonly"] = ["vx_nofold_", "vx_norank_", "vx_noplace_", "vx_noreorder_"]
+PATCHES["vx_noreorder_"] = [("voxel.hip", "    if (!ar) {   // the window's events into run order in place", "    if (false) {   // the window's events into run order in place")]
+COMBOS["vx_sortonly"] = ["vx_nofold_", "vx_norank_", "vx_noreorder_"]
+# the gather's loads only: the window's copies read, nothing counted
+PATCHES["vx_loadonly_"] = [("voxel.hip", "        atomicAdd(&L.off[run_of(ev)], 1);", "        if (ev.x == 12345.f) atomicAdd(&L.off[0], 1);")]
+COMBOS["vx_loadonly"] = ["vx_nofold_", "vx_norank_", "vx_noreorder_", "vx_noplace_", "vx_loadonly_"]
 # bitwise: 384 window events in LDS (more tiles per CU, more windows on the arena path)
 PATCHES["vx_cap384"] = [("voxel.hip", "constexpr int VB_CAP = 512;", "constexpr int VB_CAP = 384;")]
 
