@@ -280,6 +280,8 @@ def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
     with torch.no_grad():
         fused = run(lambda c: blk.lookup_conv1x1_relu(c, wgt, bias, mode="fused"))
         split = run(lambda c: blk.lookup_conv1x1_relu(c, wgt, bias, mode="split"))
+        presplit = run(lambda c: blk.lookup_conv1x1_relu(c, wgt, bias, mode="presplit"))   # column scales: once
+        presplit_ran = blk._colscale is not None
         unfused = run(lambda c: torch.relu(F.conv2d(blk(c), wgt, bias)))
         lookup = run(lambda c: blk(c))
         corr = torch.empty((B, 324, H, W), device=device)
@@ -296,12 +298,30 @@ def measure_fused_convc1(blk, coords, B, H, W, device, reps=3):
                 256, out.data_ptr(), _lib.stream_of(corr)), "split conv")
         conv = run(conv_fn(qmax))
         conv_pre = run(conv_fn(None))
+        conv_presplit = None
+        if presplit_ran:   # the presplit conv alone on one presplit lookup (ABI 16)
+            import ctypes
+            nb = ctypes.c_int64()
+            _lib.check(_lib.lib().ecorr_presplit_size(B, 4, Q, ctypes.byref(nb)), "presplit size")
+            pin = torch.empty(nb.value, dtype=torch.uint8, device=device)
+            _lib.check(_lib.lib().ecorr_lookup_presplit(blk._pyramid.data_ptr(), coords[0].contiguous().data_ptr(), B,
+                                                        H, W, Q, 4, 4, blk._colscale.data_ptr(), pin.data_ptr(),
+                                                        _lib.stream_of(pin)), "presplit lookup")
+            pkp = _lib.packed_conv1x1_weight(wgt, 256, 324, "presplit", _lib.stream_of(wgt), {})
+            conv_presplit = run(lambda c: _lib.check(_lib.lib().ecorr_conv1x1_relu_presplit(
+                pin.data_ptr(), B, 4, Q, blk._colscale.data_ptr(), pkp.data_ptr(), bias.data_ptr(), 256,
+                out.data_ptr(), _lib.stream_of(pin)), "presplit conv"))
     flops = 2.0 * B * Q * 256 * 324
     conv_bytes = 4.0 * B * Q * (324 + 256)
     default = os.environ.get("ECORR_CONVC1", "split")
     best = split if default == "split" else fused
     return {"mode": default, "ms_per_iter": round(best, 4),
             "split_ms_per_iter": round(split, 4), "fused_ms_per_iter": round(fused, 4),
+            "presplit_ms_per_iter": round(presplit, 4) if presplit_ran else None,
+            "presplit_conv_ms": round(conv_presplit, 4) if conv_presplit is not None else None,
+            "presplit_note": "mode='presplit' (ABI 16): the lookup writes corr as f16 hi + lo under a per-query "
+                             "bound scale, the conv loads it whole (no split, no maxima); not the default: the "
+                             "lookup's split costs what the conv saves (DESIGN.md §3.3)",
             "unfused_ms_per_iter": round(unfused, 4), "lookup_ms_per_iter": round(lookup, 4),
             "speedup_vs_unfused": round(unfused / best, 3),
             "fp32_equiv": {"achieved": round(flops / (best * 1e-3) / 1e12, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
@@ -442,8 +462,8 @@ def measure_voxel(device, n=1_000_000, C=15, H=480, W=640, reps=5):
     return {"ms_per_call": round(ours, 4), "events": n, "grid": [C, H, W],
             "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4),
-            "work_per_launch": f"{nbytes:.4g} B (events in + grid out; the counting sort's key-range passes "
-                               "and the ordered gather are not algorithmic bytes)",
+            "work_per_launch": f"{nbytes:.4g} B (events in + grid out; the bucketing of the events into "
+                               "tile windows, 1.33 copies each, and the windows' reads are not algorithmic bytes)",
             "events_per_s": round(n / (ours * 1e-3), 1),
             "reference_ops_on_gpu_ms": round(ref_gpu, 3), "reference_ops_on_1_cpu_core_ms": round(ref_cpu, 1),
             "speedup_vs_reference_gpu": round(ref_gpu / ours, 2),

@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see above)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libecorr.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 MAX_LEVELS = 16
 
 ECORR_OK = 0
@@ -60,6 +60,14 @@ SYMBOLS = {
     "ecorr_conv1x1_relu_split": (_i, [_p, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p]),
     # as ecorr_lookup + qmax[B][3*levels][q_count] (before stream)
     "ecorr_lookup_qmax": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+    # presplit convc1 (ABI 16): (fmap1, fmap2, B, D, H, W, scale[B*H*W + B], stream)
+    "ecorr_split_column_scale": (_i, [_p, _p, _i, _i, _i, _i, _p, _p]),
+    "ecorr_presplit_size": (_i, [_i, _i, _i, ctypes.POINTER(_i64)]),
+    # (pyramid, coords, B, H, W, q_count, levels, radius, scale, out, stream)
+    "ecorr_lookup_presplit": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+    "ecorr_conv1x1_split_pack_presplit": (_i, [_p, _i, _i, _p, _p]),
+    # (in, B, levels, Q, scale, packed, bias, O, out, stream)
+    "ecorr_conv1x1_relu_presplit": (_i, [_p, _i, _i, _i, _p, _p, _p, _i, _p, _p]),
     "ecorr_bilinear_sampler": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p, _p, _p]),
     "ecorr_coords_grid": (_i, [_i, _i, _i, _p, _p]),
     # (chunks, chunk, world, B, C, H, W, out, stream)
@@ -242,10 +250,15 @@ def packed_conv1x1_weight(weight, O, C, kind, st, cache):
         return ent[2]
     wt = weight.reshape(O, C).contiguous()
     n = ctypes.c_int64()
-    if kind == "split":
+    if kind in ("split", "presplit"):
         check(lib().ecorr_conv1x1_split_size(O, C, ctypes.byref(n)), "convc1 split weight pack")
         packed = torch.empty(n.value, dtype=torch.uint8, device=weight.device)
-        check(lib().ecorr_conv1x1_split_pack(wt.data_ptr(), O, C, packed.data_ptr(), st), "convc1 split weight pack")
+        if kind == "split":
+            check(lib().ecorr_conv1x1_split_pack(wt.data_ptr(), O, C, packed.data_ptr(), st),
+                  "convc1 split weight pack")
+        else:   # the columns in the presplit corr's channel order (C = 81 * levels)
+            check(lib().ecorr_conv1x1_split_pack_presplit(wt.data_ptr(), O, C // 81, packed.data_ptr(), st),
+                  "convc1 presplit weight pack")
     else:
         check(lib().ecorr_conv1x1_packed_size(O, C, ctypes.byref(n)), "convc1 weight pack")
         packed = torch.empty(n.value, dtype=torch.float32, device=weight.device)

@@ -27,7 +27,9 @@ corr_pyramid is a materialized COPY in the reference layout: 4 levels of B*H*W q
 (1.96 GB at DSEC B=16, the whole pyramid again), made on first access and cached on the block.
 Nothing on the E-RAFT path reads it; access it only for inspection or tests.
 """
+import ctypes
 import os
+import weakref
 
 import torch
 
@@ -42,6 +44,13 @@ def _require_device_f32(name, t):
         raise RuntimeError(f"{name} is on {t.device}: eraft_amd runs only on HIP devices (no CPU path)")
     if t.dtype != torch.float32:
         raise TypeError(f"{name} must be float32 (got {t.dtype})")
+
+
+def _version(t):
+    try:
+        return t._version
+    except RuntimeError:   # inference tensor: no version counter (and no in-place updates)
+        return -1
 
 
 def _no_grad_inputs(*ts):
@@ -79,6 +88,11 @@ class CorrBlock:
         self._rows = B * Q
         self._levels_cache = None
         self._wcache = {}   # packed convc1 weights of this block (_lib.packed_conv1x1_weight)
+        # presplit convc1: the column scales come from the fmaps (ecorr_split_column_scale), computed
+        # on the first presplit call; weak references and version counters, so the block neither
+        # keeps the fmaps alive nor trusts them after an in-place change (then: the split mode)
+        self._fmap_refs = (weakref.ref(fmap1), weakref.ref(fmap2), _version(fmap1), _version(fmap2))
+        self._colscale = None
 
     @property
     def corr_pyramid(self):
@@ -117,11 +131,16 @@ class CorrBlock:
           "split"  ecorr_lookup_qmax into a temporary [B, C, H, W] (+ per-query maxima), then
                    ecorr_conv1x1_relu_split (f16 matrix cores, split operands: normwise within 1e-5
                    of the fp32 conv);
+          "presplit" (ABI 16, radius 4, <= 4 levels) ecorr_lookup_presplit writes corr already split
+                   (f16 hi + lo under a per-query bound scale from the fmaps, ecorr_split_column_scale,
+                   once per block) and ecorr_conv1x1_relu_presplit loads it whole: normwise within 1e-5;
+                   falls back to "split" when the fmaps are gone or changed in place since the build;
+                   measured no faster than "split" (DESIGN.md §3.3);
           "fused"  ecorr_lookup_conv1x1_relu_packed: one kernel, the lookup tile never leaves the
                    CU, an exact c-ordered fp32 MFMA sum (radius 4, num_levels <= 4, O a multiple of 64)."""
         mode = mode or os.environ.get("ECORR_CONVC1", "split")
-        if mode not in ("split", "fused"):
-            raise ValueError(f"mode {mode!r}: expected 'split' or 'fused'")
+        if mode not in ("split", "presplit", "fused"):
+            raise ValueError(f"mode {mode!r}: expected 'split', 'presplit' or 'fused'")
         B, _, H, W = self._shape
         _require_device_f32("coords", coords)
         _require_device_f32("weight", weight)
@@ -147,7 +166,23 @@ class CorrBlock:
         with _lib.on_device(self._device):
             out = torch.empty((B, O, H, W), dtype=torch.float32, device=self._device)
             st = _lib.stream_of(coords)
-            if mode == "split":
+            if mode == "presplit":
+                scale = self._column_scale(st) if self.radius == 4 and self.num_levels <= 4 else None
+                if scale is None:
+                    mode = "split"
+            if mode == "presplit":
+                wt = _lib.packed_conv1x1_weight(weight, O, C, "presplit", st, self._wcache)   # once per block
+                nbytes = ctypes.c_int64()
+                _lib.check(_lib.lib().ecorr_presplit_size(B, self.num_levels, H * W, ctypes.byref(nbytes)),
+                           "CorrBlock presplit size")
+                corr = torch.empty(nbytes.value, dtype=torch.uint8, device=self._device)
+                _lib.check(_lib.lib().ecorr_lookup_presplit(
+                    self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, self.num_levels, self.radius,
+                    scale.data_ptr(), corr.data_ptr(), st), "CorrBlock lookup (presplit convc1)")
+                _lib.check(_lib.lib().ecorr_conv1x1_relu_presplit(
+                    corr.data_ptr(), B, self.num_levels, H * W, scale.data_ptr(), wt.data_ptr(), bptr, O,
+                    out.data_ptr(), st), "CorrBlock lookup+conv1x1+relu (presplit)")
+            elif mode == "split":
                 wt = _lib.packed_conv1x1_weight(weight, O, C, "split", st, self._wcache)   # once per block
                 G = 3 * self.num_levels
                 corr = torch.empty((B, C, H, W), dtype=torch.float32, device=self._device)
@@ -164,6 +199,22 @@ class CorrBlock:
                     self._pyramid.data_ptr(), coords.data_ptr(), B, H, W, H * W, self.num_levels,
                     self.radius, wt.data_ptr(), bptr, O, out.data_ptr(), st), "CorrBlock lookup+conv1x1+relu")
         return out
+
+    def _column_scale(self, st):
+        """int[B*H*W + B]: the presplit column exponents (ecorr_split_column_scale), once per block;
+        None when the fmaps are gone or were changed in place since the build."""
+        if self._colscale is None:
+            r1, r2, v1, v2 = self._fmap_refs
+            f1, f2 = r1(), r2()
+            if f1 is None or f2 is None or _version(f1) != v1 or _version(f2) != v2:
+                return None
+            B, D, H, W = self._shape
+            sc = torch.empty(B * H * W + B, dtype=torch.int32, device=self._device)
+            _lib.check(_lib.lib().ecorr_split_column_scale(f1.data_ptr(), f2.data_ptr(), B, D, H, W, sc.data_ptr(),
+                                                           st), "CorrBlock presplit column scale")
+            self._colscale = sc
+            self._fmap_refs = None
+        return self._colscale
 
     @staticmethod
     def corr(fmap1, fmap2):

@@ -267,6 +267,46 @@ ECORR_EXPORT int ecorr_conv1x1_relu_split(const float* in, int B, int C, int Q, 
     return launch_conv1x1_relu_split(in, B, C, Q, qmax, G, packed, bias, O, out, (hipStream_t)stream);
 }
 
+ECORR_EXPORT int ecorr_split_column_scale(const float* fmap1, const float* fmap2, int B, int D, int H, int W,
+                                          int* scale, void* stream) {
+    if (!fmap1 || !fmap2 || !scale) return ECORR_EINVAL;
+    return launch_split_column_scale(fmap1, fmap2, B, D, H, W, scale, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_presplit_size(int B, int levels, int q_count, int64_t* bytes) {
+    if (!bytes || B <= 0 || q_count <= 0) return ECORR_EINVAL;
+    if (levels < 1 || levels > 4) return ECORR_ELEVELS;
+    *bytes = (int64_t)B * presplit_bytes_per_item(81 * levels, q_count);
+    return ECORR_OK;
+}
+
+ECORR_EXPORT int ecorr_lookup_presplit(const float* pyramid, const float* coords, int B, int H, int W, int q_count,
+                                       int levels, int radius, const int* scale, void* out, void* stream) {
+    if (!scale || !out) return ECORR_EINVAL;
+    if (radius != 4) return ECORR_ERADIUS;
+    if (levels < 1 || levels > 4) return ECORR_ELEVELS;
+    LookupParams P{};
+    const int st = lookup_params(pyramid, coords, B, H, W, q_count, levels, radius, (float*)out, &P);
+    if (st != ECORR_OK) return st;
+    if (presplit_bytes_per_item(P.C, q_count) >= 0x7fffffffLL) return ECORR_EINVAL;   // 32-bit store offsets
+    P.scale = scale;
+    return launch_lookup(P, B, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_conv1x1_split_pack_presplit(const float* weight, int O, int levels, void* packed,
+                                                   void* stream) {
+    if (!weight || !packed) return ECORR_EINVAL;
+    if (levels < 1 || levels > 4) return ECORR_ELEVELS;
+    return launch_conv1x1_split_pack(weight, O, 81 * levels, packed, (hipStream_t)stream, levels);
+}
+
+ECORR_EXPORT int ecorr_conv1x1_relu_presplit(const void* in, int B, int levels, int Q, const int* scale,
+                                             const void* packed, const float* bias, int O, float* out, void* stream) {
+    if (!in || !packed || !out || !scale) return ECORR_EINVAL;
+    if (levels < 1 || levels > 4) return ECORR_ELEVELS;
+    return launch_conv1x1_relu_presplit(in, B, 81 * levels, Q, scale, packed, bias, O, out, (hipStream_t)stream);
+}
+
 ECORR_EXPORT int ecorr_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,
                                         int Hg, int Wg, float* out, float* mask, void* stream) {
     if (!img || !coords || !out || N <= 0 || C < 0 || h <= 0 || w <= 0 || Hg <= 0 || Wg <= 0)

@@ -75,9 +75,10 @@ __device__ __forceinline__ void split8(const float (&v)[8], float s, halfx8& hi,
 // Packed weight: for output block ob (256 channels) and chunk c, 16 KB at (ob nkc + c) SCHUNK:
 // [row block rb][hi | lo][lane l][8 halves] = W[256 ob + 32 rb + (l & 31)][16 c + 8 (l >> 5) + j]
 // scaled by 2^e_o and split (zeros past O or C) -- the v_mfma_f32_32x32x16_f16 A fragment of lane l;
-// then the int exponents e_o of all nob * 256 rows.  One workgroup per output block.
+// then the int exponents e_o of all nob * 256 rows.  One workgroup per output block.  perm_levels:
+// K position 16 c + 8 (l >> 5) + j holds channel presplit_chan(position) (the presplit corr order).
 __global__ __launch_bounds__(SNT) void split_pack_kernel(const float* __restrict__ wt, int O, int C,
-                                                         char* __restrict__ packed) {
+                                                         char* __restrict__ packed, int perm_levels) {
     __shared__ float sc[SO];
     const int ob = blockIdx.x, nob = gridDim.x, nkc = split_chunks(C), t = threadIdx.x;
     const int o = ob * SO + t;
@@ -94,7 +95,10 @@ __global__ __launch_bounds__(SNT) void split_pack_kernel(const float* __restrict
         const int r = rb * 32 + (l & 31), oo = ob * SO + r, k0 = c * SKC + 8 * (l >> 5);
         float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (oo < O && k0 + j < C) ? wt[(int64_t)oo * C + k0 + j] : 0.f;
+        for (int j = 0; j < 8; ++j) {
+            const int ch = perm_levels ? presplit_chan(k0 + j, perm_levels) : (k0 + j < C ? k0 + j : -1);
+            v[j] = (oo < O && ch >= 0) ? wt[(int64_t)oo * C + ch] : 0.f;
+        }
         halfx8 hi, lo;
         split8(v, sc[r], hi, lo);
         *reinterpret_cast<halfx8*>(base + (int64_t)i * 16) = part ? lo : hi;
@@ -112,12 +116,16 @@ __device__ __forceinline__ void wait_vm() {
 // 63.9 vs 53.9 us, profiles/r04_lab/r4l_ab_conv.txt), three buffers, two chunks ahead, with static
 // vmcnt waits (tests/test_isa_waits.py replays them on the emitted ISA); the query columns are
 // loaded PD chunks ahead into PD + 1 fixed register sets.
-template <int PD>
+// PRE: `in` is the presplit corr (ecorr_lookup_presplit): the B fragment of chunk c is two 16-byte
+// loads (hi, lo of group 2 c + kh) instead of 8 dword loads and the split, and the query exponent
+// comes from `scale` (qmax unused); the weight columns are packed in the presplit order.
+template <int PD, bool PRE = false>
 __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restrict__ in, int C, int Q,
                                                             const float* __restrict__ qmax, int G,
                                                             const char* __restrict__ packed,
                                                             const float* __restrict__ bias, int O,
-                                                            float* __restrict__ out) {
+                                                            float* __restrict__ out,
+                                                            const int* __restrict__ scale) {
     constexpr int NB = 3;
     // ALL LDS in one object: with a second __shared__ object hipcc waits vmcnt(0) before every
     // ds_read while an LDS-DMA is in flight (cdna_hip_programming.md, the second-__shared__ trap)
@@ -139,17 +147,34 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
     // corr / out of batch item b as range-checked buffers: a lane past Q starts at the end of the
     // range (every access then reads 0 / is dropped), channels past C or O fall outside by
     // themselves -- no branches around the loads and stores
-    const __amdgpu_buffer_rsrc_t csrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(in + (int64_t)b * C * Q), 0, C * Q * 4, 0x00020000);
-    const int cbase = (qok ? q : C * Q) * 4, qs = Q * 4;
+    const int qs = Q * 4;
+    // presplit: groups from ceil(C / 8) on lie past the range (zeros); a lane past Q starts past it
+    const int prange = PRE ? (C + 7) / 8 * 2 * Q * 16 : 0;
+    const __amdgpu_buffer_rsrc_t csrc = PRE
+        ? __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(reinterpret_cast<const char*>(in)) +
+                                                (int64_t)b * presplit_bytes_per_item(C, Q), 0, prange, 0x00020000)
+        : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in + (int64_t)b * C * Q), 0, C * Q * 4, 0x00020000);
+    const int cbase = PRE ? (qok ? q * 16 : prange) + kh * 2 * Q * 16 : (qok ? q : C * Q) * 4;
     const char* wsrc = packed + (int64_t)ob * nkc * SCHUNK;
 
-    // B fragment of chunk c: corr[b][16 c + 8 kh + j][q], j = 0..7 (zeros past C or Q)
+    // B fragment of chunk c: corr[b][16 c + 8 kh + j][q], j = 0..7 (zeros past C or Q); presplit:
+    // v[0..3] = the hi halves, v[4..7] = the lo halves of group 2 c + kh (chunk offset in soffset)
     auto load_b = [&](int c, float (&v)[8]) __attribute__((always_inline)) {
-        const int off = cbase + (c * SKC + 8 * kh) * qs;
+        if constexpr (PRE) {
+            typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+            const u4 h = __builtin_amdgcn_raw_buffer_load_b128(csrc, cbase, c * 4 * Q * 16, 0);
+            const u4 l = __builtin_amdgcn_raw_buffer_load_b128(csrc, cbase + Q * 16, c * 4 * Q * 16, 0);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, off + j * qs, 0, 0));
+            for (int j = 0; j < 4; ++j) {
+                v[j] = __uint_as_float(h[j]);
+                v[4 + j] = __uint_as_float(l[j]);
+            }
+        } else {
+            const int off = cbase + (c * SKC + 8 * kh) * qs;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(csrc, off + j * qs, 0, 0));
+        }
     };
 
     // wave w copies the chunk's 1-KB pieces w, w + 4, w + 8, w + 12 (lane-linear, as LDS-DMA writes
@@ -178,14 +203,19 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
     const __amdgpu_buffer_rsrc_t brs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bias), 0, bias ? O * 4 : 0, 0x00020000);
     const float bo_t = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (ob * SO + tid) * 4, 0, 0));
-    constexpr int QG = 6;   // partial maxima per wave and pass (G = 12 for 4 levels: one pass)
+    constexpr int QG = PRE ? 1 : 6;   // partial maxima per wave and pass (G = 12 for 4 levels: one pass)
     const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(qmax ? qmax + (int64_t)b * G * Q : nullptr), 0, qmax ? G * Q * 4 : 0, 0x00020000);
     const int qc = min(q, Q - 1);
     float qv[QG];
+    int eq = 0;
+    if constexpr (PRE) {   // used only by the epilogue: no wait for it here
+        eq = scale[(int64_t)b * Q + qc];
+    } else {
 #pragma unroll
-    for (int i = 0; i < QG; ++i)
-        qv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(qrs, (min(oh + 2 * i, G - 1) * Q + qc) * 4, 0, 0));
+        for (int i = 0; i < QG; ++i)
+            qv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(qrs, (min(oh + 2 * i, G - 1) * Q + qc) * 4, 0, 0));
+    }
     __builtin_amdgcn_sched_barrier(0);
     sex[tid] = eo_t;
     sbias[tid] = bo_t;
@@ -193,7 +223,8 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
     // ---- the query's largest |value| over C -> its exponent: from the lookup's partial maxima
     // (ecorr_lookup_qmax; clamped repeats are harmless) or a pre-pass over the column
     float m = 0.f;
-    if (qmax) {
+    if constexpr (PRE) {
+    } else if (qmax) {
 #pragma unroll
         for (int i = 0; i < QG; ++i) m = fmaxf(m, qv[i]);
         for (int g = oh + 2 * QG; g < G; g += 2)
@@ -210,14 +241,19 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
 #pragma unroll
             for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[k][j]));
     }
-    m = fmaxf(m, __shfl_xor(m, 32));
-    if (kh == 0) red[oh][qi] = m;
+    if constexpr (!PRE) {
+        m = fmaxf(m, __shfl_xor(m, 32));
+        if (kh == 0) red[oh][qi] = m;
+    }
     __builtin_amdgcn_sched_barrier(0);
-    wait_vm<4 + 8 * PD>();   // chunk 0's pieces (chunk 1's 4 and PD x 8 B loads may be in flight)
+    // chunk 0's pieces (chunk 1's 4 and the PD chunks' B loads may be in flight; presplit: and the
+    // exponent load, issued last)
+    if constexpr (PRE) wait_vm<4 + 2 * PD + 1>();
+    else wait_vm<4 + 8 * PD>();
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): red / sex / sbias written
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    const int eq = split_exponent(fmaxf(red[0][qi], red[1][qi]));
+    if constexpr (!PRE) eq = split_exponent(fmaxf(red[0][qi], red[1][qi]));
     const float sq = pow2(eq);
 
     floatx16 acc[4];
@@ -236,7 +272,15 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
         issue_w(min(c + 2, nkc - 1), (c + 2) % NB);   // past the last chunk a harmless repeat
         __builtin_amdgcn_sched_barrier(0);   // issued here, ahead of this chunk's work
         halfx8 bh, bl;
-        split8(cur, sq, bh, bl);
+        if constexpr (PRE) {
+            typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+            bh = __builtin_bit_cast(halfx8, u4{__float_as_uint(cur[0]), __float_as_uint(cur[1]), __float_as_uint(cur[2]),
+                                               __float_as_uint(cur[3])});
+            bl = __builtin_bit_cast(halfx8, u4{__float_as_uint(cur[4]), __float_as_uint(cur[5]), __float_as_uint(cur[6]),
+                                               __float_as_uint(cur[7])});
+        } else {
+            split8(cur, sq, bh, bl);
+        }
         const char* wb = wbuf[c % NB] + lane * 16;
         // A fragments double-buffered: tile i + 2's pair is read right after tile i's MFMAs issue, so
         // the LDS latency hides behind them (read just before use: 55.5 vs 52.0 us at DSEC B = 16,
@@ -266,6 +310,8 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
         __builtin_amdgcn_sched_barrier(0);
         if (tail)
             wait_vm<4>();   // (stricter than needed if the loads were kept: still correct)
+        else if constexpr (PRE)
+            wait_vm<6>();
         else
             wait_vm<12>();
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
@@ -312,9 +358,11 @@ int64_t conv1x1_split_bytes(int O, int C) {
     return (int64_t)split_oblocks(O) * split_chunks(C) * SCHUNK + (int64_t)split_oblocks(O) * SO * 4;
 }
 
-int launch_conv1x1_split_pack(const float* wt, int O, int C, void* packed, hipStream_t stream) {
+int launch_conv1x1_split_pack(const float* wt, int O, int C, void* packed, hipStream_t stream, int perm_levels) {
     if (O <= 0 || C <= 0 || split_oblocks(O) > 65535) return ECORR_EINVAL;
-    hipLaunchKernelGGL(split_pack_kernel, dim3(split_oblocks(O)), dim3(SNT), 0, stream, wt, O, C, (char*)packed);
+    if (perm_levels && (perm_levels < 1 || perm_levels > 4 || C != 81 * perm_levels)) return ECORR_EINVAL;
+    hipLaunchKernelGGL(split_pack_kernel, dim3(split_oblocks(O)), dim3(SNT), 0, stream, wt, O, C, (char*)packed,
+                       perm_levels);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
 }
@@ -330,8 +378,23 @@ int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const float*
         return ECORR_EINVAL;
     if ((const void*)in == (const void*)out) return ECORR_EINVAL;
     const dim3 grid((unsigned)((Q + SQ - 1) / SQ), (unsigned)split_oblocks(O), (unsigned)B);
-    hipLaunchKernelGGL(conv1x1_split_kernel<kConvPD>, grid, dim3(SNT), 0, stream, in, C, Q, qmax, G,
-                       (const char*)packed, bias, O, out);
+    hipLaunchKernelGGL((conv1x1_split_kernel<kConvPD, false>), grid, dim3(SNT), 0, stream, in, C, Q, qmax, G,
+                       (const char*)packed, bias, O, out, nullptr);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
+}
+
+int launch_conv1x1_relu_presplit(const void* in, int B, int C, int Q, const int* scale, const void* packed,
+                                 const float* bias, int O, float* out, hipStream_t stream) {
+    if (B <= 0 || C <= 0 || Q <= 0 || O <= 0 || B > 65535 || split_oblocks(O) > 65535 || !scale) return ECORR_EINVAL;
+    // 32-bit buffer offsets: a lane past Q reads from the range's end on, up to PD + 1 chunks past C
+    if (presplit_bytes_per_item(C, Q) + (int64_t)(kConvPD + 2) * 4 * Q * 16 >= 0x7fffffffLL ||
+        (int64_t)(O + split_oblocks(O) * SO) * Q * 4 >= 0x7fffffffLL)
+        return ECORR_EINVAL;
+    if ((const void*)in == (const void*)out) return ECORR_EINVAL;
+    const dim3 grid((unsigned)((Q + SQ - 1) / SQ), (unsigned)split_oblocks(O), (unsigned)B);
+    hipLaunchKernelGGL((conv1x1_split_kernel<kConvPD, true>), grid, dim3(SNT), 0, stream, (const float*)in, C, Q,
+                       nullptr, 0, (const char*)packed, bias, O, out, scale);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
 }

@@ -57,7 +57,10 @@ __global__ __launch_bounds__(4 * QB) void lookup_staged(LookupParams P) {
 // PAIR (every level width even): windows staged as 8-byte column pairs (lookup_stage.h).
 // QMAX: also the query's largest |sample| over this wave's columns of the level (fmaxf: NaN
 // ignored) -> P.qmax[b][3 lv + part][p], the split convc1's column exponent without a re-read.
-template <int R, int QB, bool PAIR, bool QMAX = false>
+// PRESPLIT (radius 4): the samples scaled by 2^scale[b][p] and split into f16 hi + lo, written in the
+// presplit layout (ecorr_internal.h): the wave's 27 channels as three whole 16-byte groups (hi, lo)
+// plus 3 halves packed after all waves' groups -- the conv reads them as its B fragments.
+template <int R, int QB, bool PAIR, bool QMAX = false, bool PRESPLIT = false>
 __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
     constexpr int NTQ = 3 * QB, K = 2 * R + 1, AP = K / 3;
     static_assert(K % 3 == 0 && QB == kWave, "one wave per part, whole columns per part");
@@ -111,6 +114,54 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
 
     const int md = org[2] & 0xff;
     if (md == 2) return;   // past the range (no barrier follows)
+    static_assert(!PRESPLIT || (R == 4 && !QMAX), "presplit: radius 4, 27 channels per wave");
+    float vv[PRESPLIT ? K * AP : 1];   // presplit: the wave's 27 samples, k = 9 ai + bb
+    // presplit stores: groups g = 9 lv + 3 part + j (k = 8 j .. 8 j + 7), each written as soon as its
+    // 8th sample exists (their registers die there: 95 -> 144 VGPRs when all 27 stayed live), then
+    // the halves k = 24 .. 26 at positions 72 L + 9 lv + 3 part + i; default store policy (the conv
+    // reads them right back).  Wide stores keep soffset = 0 (tests/test_isa_store_hazard.py).
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const int64_t pbytes = PRESPLIT ? presplit_bytes_per_item(P.C, P.q_count) : 0;
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<char*>(P.out) + (int64_t)b * pbytes, 0, (int)pbytes, 0x00020000);
+    const float psc = PRESPLIT ? __int_as_float((P.scale[(int64_t)b * P.q_count + p] + 127) << 23) : 0.0f;
+    auto put = [&](int k, float v) __attribute__((always_inline)) {
+        vv[k] = v;
+        const int Q = P.q_count;
+        if (k % 8 == 7 && k < 24) {
+            const int j = k / 8;
+            h8 hi, lo;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const float x = __fmul_rn(vv[8 * j + t], psc);
+                const _Float16 h = (_Float16)x;
+                hi[t] = h;
+                lo[t] = (_Float16)__fsub_rn(x, (float)h);
+            }
+            const int off = ((9 * lv + 3 * part + j) * 2 * Q + p) * 16;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, hi), prs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, lo), prs, off + Q * 16, 0, 0);
+        }
+        if (k == K * AP - 1) {
+            const int L = P.levels;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const float x = __fmul_rn(vv[24 + i], psc);
+                const _Float16 h = (_Float16)x, l = (_Float16)__fsub_rn(x, (float)h);
+                const int pos = 72 * L + 9 * lv + 3 * part + i;
+                const int off = ((pos >> 3) * 2 * Q + p) * 16 + (pos & 7) * 2;
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), prs, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, l), prs, off + Q * 16, 0, 0);
+            }
+            if (lv == L - 1 && part == 2)   // the last group's positions past C: zeros
+                for (int pos = P.C; pos < (P.C + 7) / 8 * 8; ++pos) {
+                    const int off = ((pos >> 3) * 2 * Q + p) * 16 + (pos & 7) * 2;
+                    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)0, prs, off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)0, prs, off + Q * 16, 0, 0);
+                }
+        }
+    };
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         P.out + (int64_t)b * P.C * P.q_count, 0, P.C * P.q_count * 4, 0x00020000);
     const int voff = p * 4;
@@ -134,8 +185,11 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
                 const float* c = wc + yo[bb];
                 const float v = blend(c[0], c[1], c[SW], c[SW + 1], wx[ai], wy[bb]);
                 if constexpr (QMAX) vmax = fmaxf(vmax, fabsf(v));
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
-                                                      sbase + (a * K + bb) * P.q_count * 4, kOutAux);
+                if constexpr (PRESPLIT)
+                    put(ai * K + bb, v);
+                else
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
+                                                          sbase + (a * K + bb) * P.q_count * 4, kOutAux);
             }
         }
     } else {   // coordinates that do not fit the window: exact direct gather
@@ -145,8 +199,11 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
             for (int bb = 0; bb < K; ++bb) {
                 const float v = sample_direct(P, lv, b, p, fx[ai], fy[bb], wx[ai], wy[bb]);
                 if constexpr (QMAX) vmax = fmaxf(vmax, fabsf(v));
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
-                                                      sbase + ((part * AP + ai) * K + bb) * P.q_count * 4, kOutAux);
+                if constexpr (PRESPLIT)
+                    put(ai * K + bb, v);
+                else
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, voff,
+                                                          sbase + ((part * AP + ai) * K + bb) * P.q_count * 4, kOutAux);
             }
     }
     if constexpr (QMAX)
@@ -213,6 +270,69 @@ __global__ __launch_bounds__(NT) void coords_grid_kernel(int B, int H, int W, fl
     }
 }
 
+// Presplit column exponents (ecorr_split_column_scale).  Every sample of query p (any level: pooled
+// averages and bilinear blends of level-0 values) is bounded by max_t |corr0[p][t]| <=
+// sqrt(D) m1_p M2 (Cauchy-Schwarz on |f| <= max |f|), m1_p = max_d |f1[d][p]|, M2 = max |f2| over
+// the batch item; with m < 2^(15 - split_exponent(m)) and sqrt(D) <= 2^hd the scale
+// 2^(e1 + E2 - 15 - hd) puts every sample below 2^15 (f16 max 65504: 2x headroom for rounding).
+// A loose bound only lowers the samples' magnitude, not their 22-bit hi + lo precision, until lo
+// falls under f16's normal range (scaled |x| < 2^-3).  The maxima are over finite values: a sample
+// touching a non-finite fmap value is non-finite itself (and NaNs its query in the conv, the split
+// contract), every other sample is bounded by the finite values it was made of.
+__device__ __forceinline__ int colscale_exponent(float m) {   // conv.hip split_exponent
+    int E = 0;
+    frexpf(m, &E);
+    const int e = (m > 0.f && m <= 3.4028235e38f) ? 15 - E : 0;
+    return e < -126 ? -126 : (e > 126 ? 126 : e);
+}
+
+// max |f2| (finite) per batch item as float bits (non-negative floats order as unsigned ints)
+__global__ __launch_bounds__(NT) void colscale_m2_kernel(const float* __restrict__ f2, int64_t n,
+                                                         unsigned* __restrict__ m2) {
+    __shared__ unsigned red[NT / 64];
+    const int b = blockIdx.y;
+    const float* x = f2 + (int64_t)b * n;
+    unsigned m = 0;
+    auto take = [&](float v) {   // finite values only (below)
+        const unsigned u = __float_as_uint(v) & 0x7fffffffu;
+        m = u < 0x7f800000u ? max(m, u) : m;
+    };
+    if (n % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {   // 16-byte loads
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+#pragma unroll 4
+        for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n / 4; i += (int64_t)gridDim.x * NT) {
+            const float4 v = x4[i];
+            take(v.x), take(v.y), take(v.z), take(v.w);
+        }
+    } else {
+        for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) take(x[i]);
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, d));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < NT / 64; ++w) m = max(m, red[w]);
+        atomicMax(&m2[b], m);
+    }
+}
+
+__global__ __launch_bounds__(NT) void colscale_kernel(const float* __restrict__ f1, int B, int D, int Q, int hd,
+                                                      const unsigned* __restrict__ m2, int* __restrict__ scale) {
+    const int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x;
+    if (i >= (int64_t)B * Q) return;
+    const int64_t b = i / Q, p = i - b * Q;
+    const float* x = f1 + b * D * Q + p;
+    unsigned m = 0;
+#pragma unroll 16
+    for (int d = 0; d < D; ++d) {   // 16 loads in flight per thread (coalesced over the queries)
+        const unsigned u = __float_as_uint(x[(int64_t)d * Q]) & 0x7fffffffu;
+        m = u < 0x7f800000u ? max(m, u) : m;
+    }
+    const int s = colscale_exponent(__uint_as_float(m)) + colscale_exponent(__uint_as_float(m2[b])) - 15 - hd;
+    scale[i] = s < -126 ? -126 : (s > 126 ? 126 : s);
+}
+
 inline unsigned grid_for(int64_t n) {
     const int64_t g = (n + NT - 1) / NT;
     return (unsigned)(g < 8192 ? (g > 0 ? g : 1) : 8192);
@@ -243,6 +363,11 @@ int launch_lookup(const LookupParams& P, int B, hipStream_t stream) {
     if (cols) {
         bool pair = true;   // column-pair staging: every level width even, 8-byte aligned levels
         for (int lv = 0; lv < P.levels; ++lv) pair &= P.lw[lv] % 2 == 0 && (uintptr_t)P.lvl[lv] % 8 == 0;
+        if (P.radius == 4 && P.scale) {
+            if (pair) hipLaunchKernelGGL((lookup_cols_reg<4, 64, true, false, true>), grid, dim3(192), 0, stream, P);
+            else hipLaunchKernelGGL((lookup_cols_reg<4, 64, false, false, true>), grid, dim3(192), 0, stream, P);
+            return hip_status();
+        }
         if (P.radius == 4 && P.qmax) {
             if (pair) hipLaunchKernelGGL((lookup_cols_reg<4, 64, true, true>), grid, dim3(192), 0, stream, P);
             else hipLaunchKernelGGL((lookup_cols_reg<4, 64, false, true>), grid, dim3(192), 0, stream, P);
@@ -278,6 +403,23 @@ int launch_bilinear_sampler(const float* img, int N, int C, int h, int w, const 
 int launch_coords_grid(int B, int H, int W, float* out, hipStream_t stream) {
     hipLaunchKernelGGL(coords_grid_kernel, dim3(grid_for((int64_t)B * 2 * H * W)), dim3(NT), 0, stream, B,
                        H, W, out);
+    return hip_status();
+}
+
+int launch_split_column_scale(const float* f1, const float* f2, int B, int D, int H, int W, int* scale,
+                              hipStream_t stream) {
+    const int64_t Q = (int64_t)H * W;
+    if (B <= 0 || D <= 0 || Q <= 0 || B > 65535 || Q > 0x7fffffff) return ECORR_EINVAL;
+    int hd = 0;
+    while (((int64_t)1 << (2 * hd)) < D) ++hd;   // sqrt(D) <= 2^hd
+    unsigned* m2 = reinterpret_cast<unsigned*>(scale + B * Q);
+    const hipError_t e = hipMemsetAsync(m2, 0, (size_t)B * 4, stream);
+    if (e != hipSuccess) return ECORR_EHIP - (int)e;
+    const int64_t n = (int64_t)D * Q;
+    const unsigned gx = (unsigned)std::min<int64_t>((n + NT * 64 - 1) / (NT * 64), 1024);
+    hipLaunchKernelGGL(colscale_m2_kernel, dim3(gx, B), dim3(NT), 0, stream, f2, n, m2);
+    hipLaunchKernelGGL(colscale_kernel, dim3((unsigned)((B * Q + NT - 1) / NT)), dim3(NT), 0, stream, f1, B, D, (int)Q,
+                       hd, m2, scale);
     return hip_status();
 }
 

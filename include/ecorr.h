@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECORR_ABI_VERSION 15
+#define ECORR_ABI_VERSION 16
 #define ECORR_MAX_LEVELS 16
 #define ECORR_TILE_H 4
 #define ECORR_TILE_W 8
@@ -158,6 +158,33 @@ int ecorr_conv1x1_split_size(int O, int C, int64_t* bytes);
 int ecorr_conv1x1_split_pack(const float* weight, int O, int C, void* packed, void* stream);
 int ecorr_conv1x1_relu_split(const float* in, int B, int C, int Q, const float* qmax, int G, const void* packed,
                              const float* bias, int O, float* out, void* stream);
+
+/* Presplit convc1 (ABI 16): the lookup writes corr already split for the split conv, so the conv
+ * loads each 8-channel B fragment as two 16-byte pieces and runs no split arithmetic and no maxima.
+ * The query's scale must be known before any level's samples are written, so it is a bound, not
+ * the samples' maximum: every sample of query p (level-0 values, their 2x2 averages and bilinear
+ * blends) is at most sqrt(D) * max_d |fmap1[b][d][p]| * max |fmap2[b]| in magnitude.
+ * ecorr_split_column_scale: fmap1, fmap2 float[B][D][H][W] -> scale int[B*H*W + B] (the last B
+ *   entries are scratch): scale[b*H*W + p] = s_p, with every sample of p times 2^s_p below 2^15.
+ * ecorr_presplit_size: bytes of the presplit corr of B items of Q queries, C = 81 * levels.
+ * ecorr_lookup_presplit: radius 4 (else ECORR_ERADIUS), levels <= 4 (else ECORR_ELEVELS):
+ *   ecorr_lookup's samples x 2^s_p, split into f16 hi + lo (exactly: x 2^s = hi + lo + O(2^-22)),
+ *   in the presplit layout (groups of 8 channels, 16 B per group / hi|lo / query; the channel
+ *   order of e-raft_amd/csrc/ecorr_internal.h presplit_pos).  scale as written above.
+ * ecorr_conv1x1_split_pack_presplit: ecorr_conv1x1_split_pack with the weight columns in that order
+ *   (same byte count, ecorr_conv1x1_split_size; C = 81 * levels).
+ * ecorr_conv1x1_relu_presplit: ecorr_conv1x1_relu_split's result from the presplit corr and the
+ *   same scale: normwise within 1e-5 of the fp32 conv, not bitwise the split conv (other column
+ *   scales, other channel order); the non-finite contract of ecorr_conv1x1_relu_split.
+ * Replaces: CorrBlock.__call__ (corr.py:29-50) + F.relu(self.convc1(corr)) (update.py:67,74). */
+int ecorr_split_column_scale(const float* fmap1, const float* fmap2, int B, int D, int H, int W, int* scale,
+                             void* stream);
+int ecorr_presplit_size(int B, int levels, int q_count, int64_t* bytes);
+int ecorr_lookup_presplit(const float* pyramid, const float* coords, int B, int H, int W, int q_count, int levels,
+                          int radius, const int* scale, void* out, void* stream);
+int ecorr_conv1x1_split_pack_presplit(const float* weight, int O, int levels, void* packed, void* stream);
+int ecorr_conv1x1_relu_presplit(const void* in, int B, int levels, int Q, const int* scale, const void* packed,
+                                const float* bias, int O, float* out, void* stream);
 
 /* Generic bilinear_sampler: img float[N][C][h][w], coords float[N][Hg][Wg][2] in pixels ->
  * out float[N][C][Hg][Wg]; mask (nullable) float[N][Hg][Wg] = 1 where the normalized sample

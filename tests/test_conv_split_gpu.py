@@ -164,22 +164,25 @@ def test_split_conv_nonfinite_golden(ea, levels):
             corr = blk(coords)
             split = blk.lookup_conv1x1_relu(coords, w, bias, mode="split")
             fused = blk.lookup_conv1x1_relu(coords, w, bias, mode="fused")
+            presplit = blk.lookup_conv1x1_relu(coords, w, bias, mode="presplit")
+            assert blk._colscale is not None   # the presplit path ran (scales from the finite fmap values)
     finally:
         ea._lib.set_build_mode(prev)
     corr64 = corr.double().cpu()
     ref = torch.relu(torch.einsum("oc,bchw->bohw", w.double().cpu(), corr64) + bias.double().cpu()[None, :, None, None])
     bad = ~torch.isfinite(corr64).all(dim=1)   # [B, H, W]: queries with a non-finite sample
     assert bad.any()
-    split = split.cpu().permute(0, 2, 3, 1)
-    assert torch.isnan(split[bad]).all()
     good = ~bad
     if levels == 2:
         assert good.any()
-    if good.any():
-        assert torch.isfinite(split[good]).all()
-        got_g = split[good].double()
-        ref_g = ref.permute(0, 2, 3, 1)[good]
-        assert float((got_g - ref_g).abs().max() / ref_g.pow(2).mean().sqrt()) <= 1e-5
+    for got in (split, presplit):   # the same contract for the presplit conv (ABI 16)
+        got = got.cpu().permute(0, 2, 3, 1)
+        assert torch.isnan(got[bad]).all()
+        if good.any():
+            assert torch.isfinite(got[good]).all()
+            got_g = got[good].double()
+            ref_g = ref.permute(0, 2, 3, 1)[good]
+            assert float((got_g - ref_g).abs().max() / ref_g.pow(2).mean().sqrt()) <= 1e-5
     # the fused fp32 kernel: the reference's non-finite pattern
     fused = fused.cpu().double()
     assert torch.equal(torch.isnan(fused), torch.isnan(ref)) and torch.equal(torch.isinf(fused), torch.isinf(ref))
@@ -244,3 +247,100 @@ def test_lookup_qmax_and_conv_with_it(ea, shape):
                 dst.data_ptr(), _lib.stream_of(out)), "conv")
         torch.cuda.synchronize()
         assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+# ---- presplit (ABI 16): the lookup writes corr as f16 hi + lo under a per-query bound scale,
+# the conv loads it whole (ecorr_lookup_presplit + ecorr_conv1x1_relu_presplit)
+def _lookup_conv_ref(blk, coords, w, bias):
+    corr = blk(coords).double().cpu()
+    r = torch.einsum("oc,bchw->bohw", w.double().cpu(), corr)
+    if bias is not None:
+        r = r + bias.double().cpu()[None, :, None, None]
+    return torch.relu(r), corr
+
+
+@pytest.mark.parametrize("case", ["dsec_b2", "ragged_nobias", "levels2", "levels1", "scales"])
+def test_presplit_normwise(ea, case):
+    """Normwise <= 1e-5 against the fp64 conv of the exact lookup: DSEC 60x80 (B = 2, D = 256, O = 256);
+    a ragged slab (Q = 920, O = 96, no bias); 2 and 1 levels (C = 162 / 81: other K remainders and
+    padding groups); fmaps with per-pixel scales 2^-20..2^20 (fmap1) and per-item 2^+-30 (fmap2)
+    (per output, relative to its own scale).  Also the bound itself: every sample x 2^scale below
+    2^15."""
+    from eraft_amd import _lib
+    B, D, H, W, L, O, bias_on, sc = {
+        "dsec_b2": (2, 256, 60, 80, 4, 256, True, False),
+        "ragged_nobias": (1, 64, 23, 40, 4, 96, False, False),
+        "levels2": (2, 32, 16, 24, 2, 256, True, False),
+        "levels1": (1, 32, 20, 20, 1, 64, True, False),
+        "scales": (2, 64, 24, 32, 4, 256, True, True)}[case]
+    f1 = prng.normal(261, (B, D, H, W))
+    f2 = prng.normal(262, (B, D, H, W))
+    if sc:
+        f1 = (f1 * np.exp2(np.linspace(-20, 20, H * W)).reshape(1, 1, H, W)).astype(np.float32)
+        f2 = (f2 * np.exp2(np.array([-30.0, 30.0]))[:, None, None, None]).astype(np.float32)
+    f1, f2 = torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV)
+    coords = torch.from_numpy(prng.coords_with_flow(263, B, H, W, 3.0)).to(DEV)
+    C = 81 * L
+    w = torch.from_numpy(prng.normal(264, (O, C)) * np.float32(0.05)).to(DEV)
+    bias = torch.from_numpy(prng.normal(265, (O,)) * np.float32(0.1)).to(DEV) if bias_on else None
+    with torch.no_grad():
+        blk = ea.CorrBlock(f1, f2, num_levels=L, radius=4)
+        got = blk.lookup_conv1x1_relu(coords, w, bias, mode="presplit")
+        assert blk._colscale is not None
+        ref, corr = _lookup_conv_ref(blk, coords, w, bias)
+        scale = blk._colscale[:B * H * W].view(B, 1, H, W).cpu().double()
+    scaled = corr.abs() * torch.exp2(scale)
+    assert float(scaled.max()) < 2.0 ** 15
+    d = (got.cpu().double() - ref).abs()
+    if sc:
+        # 2^100 of dynamic range across queries: a global norm is set by a few outputs' cancellation
+        # (even the exact fp32 fused kernel is 5e-5 there); judged per output against its own scale
+        # |W[o]| . |corr[:, q]| + |bias[o]|, as test_scales_and_zero_columns judges the split conv
+        own = torch.einsum("oc,bchw->bohw", w.double().cpu().abs(), corr.abs())
+        if bias is not None:
+            own = own + bias.double().cpu().abs()[None, :, None, None]
+        err = float((d / own.clamp_min(1e-300)).max())
+    else:
+        err = float(d.max() / ref.pow(2).mean().sqrt())
+    assert err <= 1e-5, err
+
+
+def test_presplit_falls_back_after_fmap_update(ea):
+    """An fmap changed in place after the build invalidates the bound: the presplit mode then runs the
+    split mode (bitwise its result); a dropped fmap likewise."""
+    B, D, H, W, O = 1, 32, 16, 16, 64
+    f1 = torch.from_numpy(prng.normal(271, (B, D, H, W))).to(DEV)
+    f2 = torch.from_numpy(prng.normal(272, (B, D, H, W))).to(DEV)
+    coords = torch.from_numpy(prng.coords_with_flow(273, B, H, W, 2.0)).to(DEV)
+    w = torch.from_numpy(prng.normal(274, (O, 324)) * np.float32(0.05)).to(DEV)
+    with torch.no_grad():
+        blk = ea.CorrBlock(f1, f2)
+        f2.mul_(3.0)
+        a = blk.lookup_conv1x1_relu(coords, w, None, mode="presplit")
+        assert blk._colscale is None
+        assert torch.equal(a, blk.lookup_conv1x1_relu(coords, w, None, mode="split"))
+        g1 = torch.from_numpy(prng.normal(275, (B, D, H, W))).to(DEV)
+        blk2 = ea.CorrBlock(g1, torch.from_numpy(prng.normal(276, (B, D, H, W))).to(DEV))   # fmap2 dropped
+        b = blk2.lookup_conv1x1_relu(coords, w, None, mode="presplit")
+        assert blk2._colscale is None
+        assert torch.equal(b, blk2.lookup_conv1x1_relu(coords, w, None, mode="split"))
+
+
+def test_presplit_rejects(ea):
+    from eraft_amd import _lib
+    x = torch.zeros(64, dtype=torch.uint8, device=DEV)
+    sc = torch.zeros(64, dtype=torch.int32, device=DEV)
+    L = _lib.lib()
+    n = ctypes_i64()
+    assert L.ecorr_presplit_size(1, 5, 64, n) == _lib.ECORR_ELEVELS
+    assert L.ecorr_lookup_presplit(x.data_ptr(), x.data_ptr(), 1, 8, 8, 64, 4, 3, sc.data_ptr(), x.data_ptr(),
+                                   None) == _lib.ECORR_ERADIUS
+    assert L.ecorr_conv1x1_split_pack_presplit(x.data_ptr(), 64, 0, x.data_ptr(), None) == _lib.ECORR_ELEVELS
+    assert L.ecorr_conv1x1_relu_presplit(x.data_ptr(), 1, 4, 64, None, x.data_ptr(), None, 64, x.data_ptr(),
+                                         None) == _lib.ECORR_EINVAL
+
+
+def ctypes_i64():
+    import ctypes
+    return ctypes.byref(ctypes.c_int64())
+

@@ -168,7 +168,9 @@ def test_checker_flags_a_hoisted_query_load(asm):
 # race when the remainder still waited vmcnt(12)).  Its K loop is
 # rolled (3 steps per trip) with a 0-2 step remainder, so the straight-line stream replayed here is
 # prologue + two trips of the loop body + both remainder steps: barriers 0 (prologue) .. 8.
-CONV = "conv1x1_split_kernelILi2EE"
+# The presplit instantiation (PRE = true, ABI 16) loads 2 16-byte pieces per chunk: vmcnt(6) at the
+# step barriers (2 loads + 4 DMA pieces newer than chunk c + 1's).
+CONVS = {"conv1x1_split_kernelILi2ELb0EE": 12, "conv1x1_split_kernelILi2ELb1EE": 6}
 
 
 @pytest.fixture(scope="module")
@@ -184,10 +186,10 @@ def conv_asm():
         return open(out).read()
 
 
-def conv_stream(s):
+def conv_stream(s, name):
     """Straight-line replay of the conv kernel: prologue, loop body twice, the remainder steps."""
-    m = re.search(r"^(_Z\S*" + re.escape(CONV) + r"\S*):", s, re.M)
-    assert m, f"{CONV} not in the listing"
+    m = re.search(r"^(_Z\S*" + re.escape(name) + r"\S*):", s, re.M)
+    assert m, f"{name} not in the listing"
     end = s.find(".Lfunc_end", m.start())
     lines = s[m.start():end].splitlines()
     # the K loop: the loop header whose body holds the MFMAs
@@ -204,16 +206,20 @@ def conv_stream(s):
     return ins(0, head) + ins(head, back + 1) * 2 + ins(back + 1, last_bar + 1)
 
 
-def test_conv_static_waits_match_issue_order(conv_asm):
-    ins = conv_stream(conv_asm)
+@pytest.mark.parametrize("name", sorted(CONVS))
+def test_conv_static_waits_match_issue_order(conv_asm, name):
+    ins = conv_stream(conv_asm, name)
     assert sum(1 for ln in ins if ln == "s_barrier") == 9
     assert sum(1 for ln in ins if is_dma(ln)) == 4 * 10   # chunks 0 .. 9, 4 pieces per wave each
+    assert any(f"vmcnt({CONVS[name]})" in ln for ln in ins)
     errs = check_loop(ins, nbuf=3, copies=4, nk=9, chunk=16384, check_offsets=False, span=1)
     assert not errs, "\n".join(errs)
 
 
-def test_conv_checker_flags_a_short_wait(conv_asm):
-    """vmcnt(12) -> vmcnt(16) at the step barriers would let chunk c + 1's pieces be in flight."""
-    ins = [ln.replace("vmcnt(12)", "vmcnt(16)") for ln in conv_stream(conv_asm)]
+@pytest.mark.parametrize("name", sorted(CONVS))
+def test_conv_checker_flags_a_short_wait(conv_asm, name):
+    """vmcnt(N) -> vmcnt(N + 4) at the step barriers would let chunk c + 1's pieces be in flight."""
+    n = CONVS[name]
+    ins = [ln.replace(f"vmcnt({n})", f"vmcnt({n + 4})") for ln in conv_stream(conv_asm, name)]
     errs = check_loop(ins, nbuf=3, copies=4, nk=9, chunk=16384, check_offsets=False, span=1)
     assert any("DMA may be in flight" in e for e in errs), errs

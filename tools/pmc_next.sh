@@ -12,7 +12,7 @@ done
 for k in conv1x1_split_kernel lookup_conv_kernel upsample_kernel splat_band_kernel lookup_cols_reg; do
   echo "== $k"; python3 tools/pmc_one.py --summary $OUT $k
 done
-# the voxel grid's ten kernels (their names carry no "voxel": prep_dsec, scan_*, fill_runs, ...),
+# the voxel grid's kernels (their names carry no "voxel": vb_count, vb_gather, ... for DSEC),
 # from a probe that runs only them
 for grp in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $grp -d $OUT/vox_$grp -o run --output-format csv -- python3 tools/prof_voxel.py 5 > $OUT/vox_$grp.log 2>&1

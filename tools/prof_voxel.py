@@ -10,11 +10,11 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VOXEL_KERNELS = ("VoxelArgs", "norm_finalize", "norm_apply", "scan_reduce", "scan_sums", "scan_apply")
+VOXEL_KERNELS = ("VoxelArgs", "VTileArgs", "norm_finalize", "norm_apply", "scan_reduce", "scan_sums", "scan_apply")
 
 if len(sys.argv) > 1 and sys.argv[1] == "--summary":
     per = collections.defaultdict(lambda: collections.defaultdict(float))
-    calls = collections.defaultdict(set)   # counter -> (file, dispatch) of the calls' prep kernels
+    calls = collections.defaultdict(set)   # counter -> (file, dispatch) of each call's first kernel
     for f in glob.glob(os.path.join(sys.argv[2], "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
@@ -22,7 +22,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--summary":
                 continue
             short = k.replace("(anonymous namespace)", "").split("(")[0].split("::")[-1]   # ecorr::(anon)::gather<true>(...)
             per[r["Counter_Name"]][short] += float(r["Counter_Value"])
-            if short.startswith("prep"):
+            if short.startswith(("prep", "vb_count")):
                 calls[r["Counter_Name"]].add((f, r["Dispatch_Id"]))
     for name, ks in sorted(per.items()):
         n = max(1, len(calls[name]))
