@@ -449,11 +449,13 @@ inline unsigned blocks_for(int64_t n) { return (unsigned)((n + NTV - 1) / NTV); 
 // them, 1.33 on average), so a tile's bucket is exactly its window, contiguous in HBM; one
 // 256-thread workgroup per tile sorts it in LDS into runs (time bin, base cell), each run by event
 // index, and folds its 64 cells from there, 4 time bins at a time:
-//   vb_count    per block of VB_EPB events: the prep arithmetic, the windows, a slot within
-//               (window, block) per copy from an LDS atomic, the block's counts -> M[block][window];
+//   vb_count    per block of VB_EPB events: the prep arithmetic, the windows, a 16-bit slot within
+//               (window, block) per copy from an LDS atomic (8 bytes per event: nothing else is
+//               kept), the block's counts -> M[block][window];
 //   vb_colscan  per window, its counts over the blocks -> prefixes (in place) and its total;
 //   vb_starts   one block: exclusive scan of the totals -> window starts S;
-//   vb_scatter  each copy's (x, y, t_norm, value) and event index to S[w] + M[blk][w] + slot;
+//   vb_scatter  the prep again from the event fields (cheaper than storing and re-reading it), each
+//               copy's (x, y, t_norm, value) and event index to S[w] + M[blk][w] + slot;
 //   vb_gather   per tile: runs counted (LDS atomics), scanned, placed, ranked by event index; then
 //               each cell folded in pass order -- the reference's serial fold, bit for bit.  A window
 //               holding more than VB_CAP events (a hot pixel, a dense stream) is read where it lies
@@ -481,9 +483,8 @@ struct VTileArgs {
     int64_t n;
     int C, H, W;
     int gy, gx, nb, nblk;   // tile grid, windows (gy * gx), count blocks
-    uint32_t* cell;    // per event: extended base cell (ey << 16 | ex), or ~0u (no window)
-    uint4* slot;       // per event: slots of its copies (own, left, up, up-left)
-    float *fa, *fb;    // per event: t_norm, value
+    uint2* slot;       // per event: 16-bit slots of its copies (own, left, up, up-left) within
+                       // (window, block): < VB_EPB; everything else vb_scatter recomputes
     uint32_t* M;       // [nblk][nb]: counts, then their prefixes over the blocks
     uint32_t* tot;     // [nb + 1]: window totals (tot[nb] = 0)
     uint32_t* S;       // [nb + 1]: window starts
@@ -503,6 +504,19 @@ __device__ __forceinline__ int vt_window(const VTileArgs& A, int ey, int ex, int
     return (ty >= 0 && ty < A.gy && tx >= 0 && tx < A.gx) ? ty * A.gx + tx : -1;
 }
 
+// dsec_utils.py:35-41 as prep_dsec: t_norm, value and the extended base cell of event e; false when
+// the event lies in no window (no pass of it lands on the grid)
+__device__ __forceinline__ bool vt_prep(const VTileArgs& A, int64_t e, float t0, float dt, float& tn, float& val,
+                                        int& ey, int& ex) {
+    tn = __fdiv_rn(__fmul_rn((float)(A.C - 1), __fsub_rn(A.t[e], t0)), dt);
+    val = __fsub_rn(__fmul_rn(2.0f, A.p[e]), 1.0f);
+    const int x0 = x86_i32(A.x[e]), y0 = x86_i32(A.y[e]), ti = x86_i32(tn);
+    ey = y0 + 1;
+    ex = x0 + 1;
+    return x0 >= -1 && x0 < A.W && y0 >= -1 && y0 < A.H && ti >= -1 && ti < A.C;
+}
+static_assert(VB_EPB <= 65536, "16-bit slots within (window, block)");
+
 __global__ __launch_bounds__(VB_CNT) void vb_count(VTileArgs A) {
     __shared__ uint32_t hist[VB_MAXNB];
     const int tid = threadIdx.x, blk = blockIdx.x;
@@ -513,24 +527,17 @@ __global__ __launch_bounds__(VB_CNT) void vb_count(VTileArgs A) {
     for (int k = 0; k < VB_EPB / VB_CNT; ++k) {
         const int64_t e = (int64_t)blk * VB_EPB + k * VB_CNT + tid;
         if (e >= A.n) break;
-        // dsec_utils.py:35-41 as prep_dsec
-        const float tn = __fdiv_rn(__fmul_rn((float)(A.C - 1), __fsub_rn(A.t[e], t0)), dt);
-        const int x0 = x86_i32(A.x[e]), y0 = x86_i32(A.y[e]), ti = x86_i32(tn);
-        A.fa[e] = tn;
-        A.fb[e] = __fsub_rn(__fmul_rn(2.0f, A.p[e]), 1.0f);
-        uint32_t cell = ~0u;
-        if (x0 >= -1 && x0 < A.W && y0 >= -1 && y0 < A.H && ti >= -1 && ti < A.C) {
-            const int ey = y0 + 1, ex = x0 + 1;
-            cell = (uint32_t)ey << 16 | (uint32_t)ex;
-            uint32_t s[4];
+        float tn, val;
+        int ey, ex;
+        if (vt_prep(A, e, t0, dt, tn, val, ey, ex)) {
+            uint32_t sl[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int w = vt_window(A, ey, ex, q);
-                s[q] = w >= 0 ? atomicAdd(&hist[w], 1u) : 0u;
+                sl[q] = w >= 0 ? atomicAdd(&hist[w], 1u) : 0u;
             }
-            A.slot[e] = make_uint4(s[0], s[1], s[2], s[3]);
+            A.slot[e] = make_uint2(sl[0] | sl[1] << 16, sl[2] | sl[3] << 16);
         }
-        A.cell[e] = cell;
     }
     __syncthreads();
     uint32_t* row = A.M + (int64_t)blk * A.nb;
@@ -582,12 +589,13 @@ __global__ __launch_bounds__(NTV) void vb_starts(VTileArgs A) {
 __global__ __launch_bounds__(NTV) void vb_scatter(VTileArgs A) {
     const int64_t e = blockIdx.x * (int64_t)NTV + threadIdx.x;
     if (e >= A.n) return;
-    const uint32_t cell = A.cell[e];
-    if (cell == ~0u) return;
-    const int ey = (int)(cell >> 16), ex = (int)(cell & 0xffff);
-    const uint4 s = A.slot[e];
-    const uint32_t sl[4] = {s.x, s.y, s.z, s.w};
-    const float4 v = make_float4(A.x[e], A.y[e], A.fa[e], A.fb[e]);
+    const float t0 = A.t[0], dt = __fsub_rn(A.t[A.n - 1], t0);
+    float tn, val;
+    int ey, ex;
+    if (!vt_prep(A, e, t0, dt, tn, val, ey, ex)) return;   // the same arithmetic as vb_count's
+    const uint2 s = A.slot[e];
+    const uint32_t sl[4] = {s.x & 0xffff, s.x >> 16, s.y & 0xffff, s.y >> 16};
+    const float4 v = make_float4(A.x[e], A.y[e], tn, val);
     const uint32_t* Mrow = A.M + (e / VB_EPB) * A.nb;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -814,17 +822,14 @@ inline int hip_status() {
 
 // Workspace of the tiled DSEC path.
 struct VTileWs {
-    size_t cell, slot, fa, fb, M, tot, S, pay, norm, part, aord, aords, total;
+    size_t slot, M, tot, S, pay, norm, part, aord, aords, total;
 };
 
 void plan_tiled(int64_t n, const VTileGeom& g, VTileWs* w) {
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t at = o; o += align256(bytes); return at; };
     const size_t copies = 4 * (size_t)n;   // an event lies in at most 4 windows
-    w->cell = take(4 * (size_t)n);
-    w->slot = take(16 * (size_t)n);
-    w->fa = take(4 * (size_t)n);
-    w->fb = take(4 * (size_t)n);
+    w->slot = take(8 * (size_t)n);
     w->M = take(4 * (size_t)g.nblk * g.nb);
     w->tot = take(4 * ((size_t)g.nb + 1));
     w->S = take(4 * ((size_t)g.nb + 1));
@@ -845,10 +850,7 @@ int launch_voxel_tiled(const float* p, const float* t, const float* x, const flo
     A.p = p; A.t = t; A.x = x; A.y = y;
     A.n = n; A.C = C; A.H = H; A.W = W;
     A.gy = g.gy; A.gx = g.gx; A.nb = g.nb; A.nblk = g.nblk;
-    A.cell = (uint32_t*)(base + w.cell);
-    A.slot = (uint4*)(base + w.slot);
-    A.fa = (float*)(base + w.fa);
-    A.fb = (float*)(base + w.fb);
+    A.slot = (uint2*)(base + w.slot);
     A.M = (uint32_t*)(base + w.M);
     A.tot = (uint32_t*)(base + w.tot);
     A.S = (uint32_t*)(base + w.S);
