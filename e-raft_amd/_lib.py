@@ -65,6 +65,7 @@ SYMBOLS = {
     "ecorr_presplit_size": (_i, [_i, _i, _i, ctypes.POINTER(_i64)]),
     # (pyramid, coords, B, H, W, q_count, levels, radius, scale, out, stream)
     "ecorr_lookup_presplit": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+    "ecorr_conv1x1_presplit_size": (_i, [_i, _i, ctypes.POINTER(_i64)]),
     "ecorr_conv1x1_split_pack_presplit": (_i, [_p, _i, _i, _p, _p]),
     # (in, B, levels, Q, scale, packed, bias, O, out, stream)
     "ecorr_conv1x1_relu_presplit": (_i, [_p, _i, _i, _i, _p, _p, _p, _i, _p, _p]),
@@ -251,7 +252,10 @@ def packed_conv1x1_weight(weight, O, C, kind, st, cache):
     wt = weight.reshape(O, C).contiguous()
     n = ctypes.c_int64()
     if kind in ("split", "presplit"):
-        check(lib().ecorr_conv1x1_split_size(O, C, ctypes.byref(n)), "convc1 split weight pack")
+        if kind == "split":
+            check(lib().ecorr_conv1x1_split_size(O, C, ctypes.byref(n)), "convc1 split weight pack")
+        else:
+            check(lib().ecorr_conv1x1_presplit_size(O, C // 81, ctypes.byref(n)), "convc1 presplit weight pack")
         packed = torch.empty(n.value, dtype=torch.uint8, device=weight.device)
         if kind == "split":
             check(lib().ecorr_conv1x1_split_pack(wt.data_ptr(), O, C, packed.data_ptr(), st),

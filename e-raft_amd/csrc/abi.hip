@@ -276,7 +276,7 @@ ECORR_EXPORT int ecorr_split_column_scale(const float* fmap1, const float* fmap2
 ECORR_EXPORT int ecorr_presplit_size(int B, int levels, int q_count, int64_t* bytes) {
     if (!bytes || B <= 0 || q_count <= 0) return ECORR_EINVAL;
     if (levels < 1 || levels > 4) return ECORR_ELEVELS;
-    *bytes = (int64_t)B * presplit_bytes_per_item(81 * levels, q_count);
+    *bytes = (int64_t)B * presplit_bytes_per_item(presplit_positions(levels), q_count);
     return ECORR_OK;
 }
 
@@ -288,9 +288,17 @@ ECORR_EXPORT int ecorr_lookup_presplit(const float* pyramid, const float* coords
     LookupParams P{};
     const int st = lookup_params(pyramid, coords, B, H, W, q_count, levels, radius, (float*)out, &P);
     if (st != ECORR_OK) return st;
-    if (presplit_bytes_per_item(P.C, q_count) >= 0x7fffffffLL) return ECORR_EINVAL;   // 32-bit store offsets
+    if (presplit_bytes_per_item(presplit_positions(levels), q_count) >= 0x7fffffffLL)
+        return ECORR_EINVAL;   // 32-bit store offsets
     P.scale = scale;
     return launch_lookup(P, B, (hipStream_t)stream);
+}
+
+ECORR_EXPORT int ecorr_conv1x1_presplit_size(int O, int levels, int64_t* bytes) {
+    if (!bytes || O <= 0) return ECORR_EINVAL;
+    if (levels < 1 || levels > 4) return ECORR_ELEVELS;
+    *bytes = conv1x1_presplit_bytes(O, levels);
+    return ECORR_OK;
 }
 
 ECORR_EXPORT int ecorr_conv1x1_split_pack_presplit(const float* weight, int O, int levels, void* packed,
@@ -304,7 +312,7 @@ ECORR_EXPORT int ecorr_conv1x1_relu_presplit(const void* in, int B, int levels, 
                                              const void* packed, const float* bias, int O, float* out, void* stream) {
     if (!in || !packed || !out || !scale) return ECORR_EINVAL;
     if (levels < 1 || levels > 4) return ECORR_ELEVELS;
-    return launch_conv1x1_relu_presplit(in, B, 81 * levels, Q, scale, packed, bias, O, out, (hipStream_t)stream);
+    return launch_conv1x1_relu_presplit(in, B, levels, Q, scale, packed, bias, O, out, (hipStream_t)stream);
 }
 
 ECORR_EXPORT int ecorr_bilinear_sampler(const float* img, int N, int C, int h, int w, const float* coords,

@@ -76,11 +76,13 @@ __device__ __forceinline__ void split8(const float (&v)[8], float s, halfx8& hi,
 // [row block rb][hi | lo][lane l][8 halves] = W[256 ob + 32 rb + (l & 31)][16 c + 8 (l >> 5) + j]
 // scaled by 2^e_o and split (zeros past O or C) -- the v_mfma_f32_32x32x16_f16 A fragment of lane l;
 // then the int exponents e_o of all nob * 256 rows.  One workgroup per output block.  perm_levels:
-// K position 16 c + 8 (l >> 5) + j holds channel presplit_chan(position) (the presplit corr order).
+// K = presplit_positions(levels) positions, position 16 c + 8 (l >> 5) + j holding channel
+// presplit_chan(position) (the presplit corr order; zeros where that is -1).
 __global__ __launch_bounds__(SNT) void split_pack_kernel(const float* __restrict__ wt, int O, int C,
                                                          char* __restrict__ packed, int perm_levels) {
     __shared__ float sc[SO];
-    const int ob = blockIdx.x, nob = gridDim.x, nkc = split_chunks(C), t = threadIdx.x;
+    const int K = perm_levels ? presplit_positions(perm_levels) : C;   // K positions (C: the row length)
+    const int ob = blockIdx.x, nob = gridDim.x, nkc = split_chunks(K), t = threadIdx.x;
     const int o = ob * SO + t;
     float m = 0.f;
     if (o < O)
@@ -148,7 +150,8 @@ __global__ __launch_bounds__(SNT) void conv1x1_split_kernel(const float* __restr
     // range (every access then reads 0 / is dropped), channels past C or O fall outside by
     // themselves -- no branches around the loads and stores
     const int qs = Q * 4;
-    // presplit: groups from ceil(C / 8) on lie past the range (zeros); a lane past Q starts past it
+    // presplit (C = K positions): groups from ceil(K / 8) on lie past the range (zeros); a lane past Q
+    // starts past it
     const int prange = PRE ? (C + 7) / 8 * 2 * Q * 16 : 0;
     const __amdgpu_buffer_rsrc_t csrc = PRE
         ? __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(reinterpret_cast<const char*>(in)) +
@@ -358,6 +361,8 @@ int64_t conv1x1_split_bytes(int O, int C) {
     return (int64_t)split_oblocks(O) * split_chunks(C) * SCHUNK + (int64_t)split_oblocks(O) * SO * 4;
 }
 
+int64_t conv1x1_presplit_bytes(int O, int levels) { return conv1x1_split_bytes(O, presplit_positions(levels)); }
+
 int launch_conv1x1_split_pack(const float* wt, int O, int C, void* packed, hipStream_t stream, int perm_levels) {
     if (O <= 0 || C <= 0 || split_oblocks(O) > 65535) return ECORR_EINVAL;
     if (perm_levels && (perm_levels < 1 || perm_levels > 4 || C != 81 * perm_levels)) return ECORR_EINVAL;
@@ -384,8 +389,9 @@ int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const float*
     return e == hipSuccess ? ECORR_OK : ECORR_EHIP - (int)e;
 }
 
-int launch_conv1x1_relu_presplit(const void* in, int B, int C, int Q, const int* scale, const void* packed,
+int launch_conv1x1_relu_presplit(const void* in, int B, int levels, int Q, const int* scale, const void* packed,
                                  const float* bias, int O, float* out, hipStream_t stream) {
+    const int C = presplit_positions(levels);   // the kernel's K: positions, zeros included
     if (B <= 0 || C <= 0 || Q <= 0 || O <= 0 || B > 65535 || split_oblocks(O) > 65535 || !scale) return ECORR_EINVAL;
     // 32-bit buffer offsets: a lane past Q reads from the range's end on, up to PD + 1 chunks past C
     if (presplit_bytes_per_item(C, Q) + (int64_t)(kConvPD + 2) * 4 * Q * 16 >= 0x7fffffffLL ||

@@ -79,36 +79,42 @@ int launch_conv1x1_pack(const float* wt, int O, int C, float* packed, hipStream_
 int64_t conv1x1_split_bytes(int O, int C);
 // perm_levels > 0: the weight columns in the presplit channel order of that many radius-4 levels
 int launch_conv1x1_split_pack(const float* wt, int O, int C, void* packed, hipStream_t stream, int perm_levels = 0);
+// the presplit pack's byte count (its K = presplit_positions(levels))
+int64_t conv1x1_presplit_bytes(int O, int levels);
 int launch_conv1x1_relu_split(const float* in, int B, int C, int Q, const float* qmax, int G, const void* packed,
                               const float* bias, int O, float* out, hipStream_t stream);
 
 // Presplit corr (ecorr_lookup_presplit -> ecorr_conv1x1_relu_presplit), radius 4, L <= 4 levels,
-// C = 81 L channels.  Channel ch = 81 lv + 27 part + k (lookup_cols_reg: wave `part` owns the 27
-// channels 9 ai + bb, k < 27) sits at K position
-//   72 lv + 24 part + k              for k < 24 (three whole 8-channel groups of one wave)
-//   72 L + 9 lv + 3 part + (k - 24)  for k >= 24 (the waves' last 3 channels, packed after them)
-// so a wave writes whole 16-byte groups but for 3 values; the conv's weight columns are permuted
-// the same way (the channel sum is order-free up to rounding).  Layout per batch item:
-// [group g < PS_NG(C)][hi | lo][query][8 halves], 16 B per (g, hi|lo, query); PS_NG is even (whole
-// 16-channel K chunks), positions C .. 8 ceil(C / 8) - 1 are written as zeros, groups from
-// ceil(C / 8) on are never written (the conv reads them out of range: zeros).
-__host__ __device__ inline int presplit_groups(int C) { return 2 * ((C + 15) / 16); }
+// C = 81 L channels at K = 88 L positions.  Channel ch = 81 lv + 27 part + k (lookup_cols_reg: wave
+// `part` owns the 27 channels 9 ai + bb, k < 27) sits at K position
+//   72 lv + 24 part + k               for k < 24 (three whole 8-channel groups of one wave)
+//   72 L + 16 lv + 3 part + (k - 24)  for k >= 24 (the level's 9 last channels, 2 groups per level:
+//                                      positions 9 .. 15 of them are zeros)
+// so every group is written whole by one wave (the leftovers through LDS, by waves 0 and 1 of the
+// level's workgroup): 2-byte stores shared between waves cost the lookup 7.5 us per call
+// (profiles/r06_lab/ab_presplit_stores.json).  The conv's weight columns are permuted the same way
+// (the channel sum is order-free up to rounding).  Layout per batch item: [group g][hi | lo][query]
+// [8 halves], 16 B per (g, hi|lo, query), presplit_groups(K) groups (even: whole 16-channel K
+// chunks); groups from 11 L on are never written (the conv reads them out of range: zeros).
+__host__ __device__ inline int presplit_positions(int L) { return 88 * L; }
+__host__ __device__ inline int presplit_groups(int K) { return 2 * ((K + 15) / 16); }
 __host__ __device__ inline int presplit_pos(int ch, int L) {
     const int lv = ch / 81, r = ch - 81 * lv, part = r / 27, k = r - 27 * part;
-    return k < 24 ? 72 * lv + 24 * part + k : 72 * L + 9 * lv + 3 * part + (k - 24);
+    return k < 24 ? 72 * lv + 24 * part + k : 72 * L + 16 * lv + 3 * part + (k - 24);
 }
-__host__ __device__ inline int presplit_chan(int pos, int L) {   // inverse; -1 past C
+__host__ __device__ inline int presplit_chan(int pos, int L) {   // inverse; -1 for a zero position
     if (pos < 72 * L) {
         const int lv = pos / 72, r = pos - 72 * lv, part = r / 24;
         return 81 * lv + 27 * part + (r - 24 * part);
     }
-    const int j = pos - 72 * L;
-    if (j >= 9 * L) return -1;
-    const int lv = j / 9, r = j - 9 * lv, part = r / 3;
+    const int j = pos - 72 * L, lv = j / 16, r = j - 16 * lv;
+    if (lv >= L || r >= 9) return -1;
+    const int part = r / 3;
     return 81 * lv + 27 * part + 24 + (r - 3 * part);
 }
-__host__ __device__ inline int64_t presplit_bytes_per_item(int C, int Q) { return (int64_t)presplit_groups(C) * 2 * Q * 16; }
-int launch_conv1x1_relu_presplit(const void* in, int B, int C, int Q, const int* scale, const void* packed,
+// bytes of one batch item's presplit corr at K positions
+__host__ __device__ inline int64_t presplit_bytes_per_item(int K, int Q) { return (int64_t)presplit_groups(K) * 2 * Q * 16; }
+int launch_conv1x1_relu_presplit(const void* in, int B, int levels, int Q, const int* scale, const void* packed,
                                  const float* bias, int O, float* out, hipStream_t stream);
 // scale[b][q] (+ B trailing scratch entries): the presplit column exponents from the fmaps (lookup.hip)
 int launch_split_column_scale(const float* f1, const float* f2, int B, int D, int H, int W, int* scale,

@@ -113,19 +113,24 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
     }
 
     const int md = org[2] & 0xff;
-    if (md == 2) return;   // past the range (no barrier follows)
+    // past the range: no barrier follows, except in the presplit form (its leftover exchange), whose
+    // lanes past the range stay to reach the barriers and store nothing (a whole wave of them: the
+    // workgroup's three waves share their queries, so all three have ended)
+    if (md == 2 && !PRESPLIT) return;
     static_assert(!PRESPLIT || (R == 4 && !QMAX), "presplit: radius 4, 27 channels per wave");
     float vv[PRESPLIT ? K * AP : 1];   // presplit: the wave's 27 samples, k = 9 ai + bb
     // presplit stores: groups g = 9 lv + 3 part + j (k = 8 j .. 8 j + 7), each written as soon as its
-    // 8th sample exists (their registers die there: 95 -> 144 VGPRs when all 27 stayed live), then
-    // the halves k = 24 .. 26 at positions 72 L + 9 lv + 3 part + i; default store policy (the conv
-    // reads them right back).  Wide stores keep soffset = 0 (tests/test_isa_store_hazard.py).
+    // 8th sample exists (their registers die there: 95 -> 144 VGPRs when all 27 stayed live); the
+    // halves k = 24 .. 26 go through LDS to the level's two leftover groups 9 L + 2 lv (+ 1), written
+    // whole by waves 0 and 1 after the exchange; default store policy (the conv reads them right
+    // back).  Wide stores keep soffset = 0 (tests/test_isa_store_hazard.py).
     typedef _Float16 h8 __attribute__((ext_vector_type(8)));
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    const int64_t pbytes = PRESPLIT ? presplit_bytes_per_item(P.C, P.q_count) : 0;
+    const int64_t pbytes = PRESPLIT ? presplit_bytes_per_item(presplit_positions(P.levels), P.q_count) : 0;
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<char*>(P.out) + (int64_t)b * pbytes, 0, (int)pbytes, 0x00020000);
-    const float psc = PRESPLIT ? __int_as_float((P.scale[(int64_t)b * P.q_count + p] + 127) << 23) : 0.0f;
+    const float psc = PRESPLIT && valid ? __int_as_float((P.scale[(int64_t)b * P.q_count + p] + 127) << 23) : 0.0f;
+    uint32_t left[3] = {0, 0, 0};   // presplit: the leftover halves, hi | lo << 16
     auto put = [&](int k, float v) __attribute__((always_inline)) {
         vv[k] = v;
         const int Q = P.q_count;
@@ -143,23 +148,11 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, hi), prs, off, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, lo), prs, off + Q * 16, 0, 0);
         }
-        if (k == K * AP - 1) {
-            const int L = P.levels;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const float x = __fmul_rn(vv[24 + i], psc);
-                const _Float16 h = (_Float16)x, l = (_Float16)__fsub_rn(x, (float)h);
-                const int pos = 72 * L + 9 * lv + 3 * part + i;
-                const int off = ((pos >> 3) * 2 * Q + p) * 16 + (pos & 7) * 2;
-                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), prs, off, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, l), prs, off + Q * 16, 0, 0);
-            }
-            if (lv == L - 1 && part == 2)   // the last group's positions past C: zeros
-                for (int pos = P.C; pos < (P.C + 7) / 8 * 8; ++pos) {
-                    const int off = ((pos >> 3) * 2 * Q + p) * 16 + (pos & 7) * 2;
-                    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)0, prs, off, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)0, prs, off + Q * 16, 0, 0);
-                }
+        if (k >= 24) {
+            const float x = __fmul_rn(v, psc);
+            const _Float16 h = (_Float16)x, l = (_Float16)__fsub_rn(x, (float)h);
+            left[k - 24] = (uint32_t)__builtin_bit_cast(unsigned short, h) |
+                           (uint32_t)__builtin_bit_cast(unsigned short, l) << 16;
         }
     };
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -192,7 +185,7 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
                                                           sbase + (a * K + bb) * P.q_count * 4, kOutAux);
             }
         }
-    } else {   // coordinates that do not fit the window: exact direct gather
+    } else if (md == 1) {   // coordinates that do not fit the window: exact direct gather
 #pragma unroll
         for (int ai = 0; ai < AP; ++ai)
 #pragma unroll
@@ -208,6 +201,26 @@ __global__ __launch_bounds__(3 * QB) void lookup_cols_reg(LookupParams P) {
     }
     if constexpr (QMAX)
         if (valid) P.qmax[((int64_t)b * 3 * P.levels + 3 * lv + part) * P.q_count + p] = vmax;
+    if constexpr (PRESPLIT) {   // the level's 9 leftover halves per query -> groups 9 L + 2 lv (+ 1)
+        __syncthreads();   // every wave's window reads done: the window buffer becomes the exchange
+        uint32_t* xch = reinterpret_cast<uint32_t*>(st.win);   // [9][QB], 2.3 KB
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xch[(3 * part + i) * QB + g] = left[i];
+        __syncthreads();
+        if (part < 2 && md != 2) {   // wave 0: leftovers 0-7, wave 1: leftover 8 + 7 zero halves
+            h8 hi, lo;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const uint32_t u = (part == 0 || t == 0) ? xch[(8 * part + t) * QB + g] : 0u;
+                hi[t] = __builtin_bit_cast(_Float16, (unsigned short)(u & 0xffff));
+                lo[t] = __builtin_bit_cast(_Float16, (unsigned short)(u >> 16));
+            }
+            const int Q = P.q_count;
+            const int off = ((9 * P.levels + 2 * lv + part) * 2 * Q + p) * 16;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, hi), prs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, lo), prs, off + Q * 16, 0, 0);
+        }
+    }
 }
 
 // Partial maxima for the lookups without a QMAX instantiation: thread = (b, query), the max of |out|

@@ -166,13 +166,15 @@ int ecorr_conv1x1_relu_split(const float* in, int B, int C, int Q, const float* 
  * blends) is at most sqrt(D) * max_d |fmap1[b][d][p]| * max |fmap2[b]| in magnitude.
  * ecorr_split_column_scale: fmap1, fmap2 float[B][D][H][W] -> scale int[B*H*W + B] (the last B
  *   entries are scratch): scale[b*H*W + p] = s_p, with every sample of p times 2^s_p below 2^15.
- * ecorr_presplit_size: bytes of the presplit corr of B items of Q queries, C = 81 * levels.
+ * ecorr_presplit_size: bytes of the presplit corr of B items of Q queries (88 * levels positions
+ *   for the 81 * levels channels).
  * ecorr_lookup_presplit: radius 4 (else ECORR_ERADIUS), levels <= 4 (else ECORR_ELEVELS):
  *   ecorr_lookup's samples x 2^s_p, split into f16 hi + lo (exactly: x 2^s = hi + lo + O(2^-22)),
- *   in the presplit layout (groups of 8 channels, 16 B per group / hi|lo / query; the channel
- *   order of e-raft_amd/csrc/ecorr_internal.h presplit_pos).  scale as written above.
- * ecorr_conv1x1_split_pack_presplit: ecorr_conv1x1_split_pack with the weight columns in that order
- *   (same byte count, ecorr_conv1x1_split_size; C = 81 * levels).
+ *   in the presplit layout (groups of 8 positions, 16 B per group / hi|lo / query; the channel
+ *   order of e-raft_amd/csrc/ecorr_internal.h presplit_pos, zeros at the 7 * levels padding
+ *   positions).  scale as written above.
+ * ecorr_conv1x1_presplit_size / ecorr_conv1x1_split_pack_presplit: ecorr_conv1x1_split_pack with the
+ *   weight columns at those positions (C = 81 * levels).
  * ecorr_conv1x1_relu_presplit: ecorr_conv1x1_relu_split's result from the presplit corr and the
  *   same scale: normwise within 1e-5 of the fp32 conv, not bitwise the split conv (other column
  *   scales, other channel order); the non-finite contract of ecorr_conv1x1_relu_split.
@@ -182,6 +184,7 @@ int ecorr_split_column_scale(const float* fmap1, const float* fmap2, int B, int 
 int ecorr_presplit_size(int B, int levels, int q_count, int64_t* bytes);
 int ecorr_lookup_presplit(const float* pyramid, const float* coords, int B, int H, int W, int q_count, int levels,
                           int radius, const int* scale, void* out, void* stream);
+int ecorr_conv1x1_presplit_size(int O, int levels, int64_t* bytes);
 int ecorr_conv1x1_split_pack_presplit(const float* weight, int O, int levels, void* packed, void* stream);
 int ecorr_conv1x1_relu_presplit(const void* in, int B, int levels, int Q, const int* scale, const void* packed,
                                 const float* bias, int O, float* out, void* stream);

@@ -88,6 +88,25 @@ with torch.no_grad():
         blk._pyramid.data_ptr(), c.data_ptr(), B, H, W, Q, 4, 4, cin.data_ptr(), qmax.data_ptr(), st))
     res["lookup_presplit_us"] = run(lambda c: _lib.lib().ecorr_lookup_presplit(
         blk._pyramid.data_ptr(), c.data_ptr(), B, H, W, Q, 4, 4, sc.data_ptr(), pin.data_ptr(), st))
+    # lab builds (AB_ALT_LIB=name=path,...): their presplit lookup and conv on the same inputs
+    for k, item in enumerate(filter(None, os.environ.get("AB_ALT_LIB", "").split(","))):
+        name, _, path = item.rpartition("=")
+        L = ctypes.CDLL(os.path.join(ROOT, path))
+        for sym, (rt, args) in _lib.SYMBOLS.items():
+            if hasattr(L, sym):
+                getattr(L, sym).restype = rt
+                getattr(L, sym).argtypes = args
+        pin2 = torch.empty_like(pin)
+        n2 = ctypes.c_int64()
+        _lib.check(L.ecorr_conv1x1_presplit_size(O, 4, ctypes.byref(n2)), "size")
+        pk2 = torch.empty(n2.value, dtype=torch.uint8, device=dev)
+        _lib.check(L.ecorr_conv1x1_split_pack_presplit(wgt.data_ptr(), O, 4, pk2.data_ptr(), st), "pack")
+        out2 = torch.empty_like(out)
+        res.setdefault("alt", {})[name or f"alt{k}"] = {
+            "lookup_presplit_us": run(lambda c: L.ecorr_lookup_presplit(
+                blk._pyramid.data_ptr(), c.data_ptr(), B, H, W, Q, 4, 4, sc.data_ptr(), pin2.data_ptr(), st)),
+            "conv_presplit_us": run(lambda c: L.ecorr_conv1x1_relu_presplit(
+                pin2.data_ptr(), B, 4, Q, sc.data_ptr(), pk2.data_ptr(), bias.data_ptr(), O, out2.data_ptr(), st))}
     blk2 = eraft_amd.CorrBlock(f1, f2)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
