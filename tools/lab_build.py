@@ -758,7 +758,19 @@ PREDIFF = {"qs": "build_qs.diff", "lkw_": "lookup_win.diff", "mo_ws": "lookup_co
            "cvt": "conv_tiles.diff"}
 
 
+# Recipes whose patch targets the tree has moved past, with the last commit they apply to (their
+# records stay under profiles/): build them from a worktree of that commit.  The presplit convc1
+# (8712df9) rewrote conv.hip's column loads and lookup.hip's store path.
+RETIRED = {n: "4dc7dd1" for n in (
+    "cv_bothoob", "cv_l2ld", "cv_soff", "cv_soff_pf3", "cvq2p1", "cvq4p1", "cvq4p2", "cvt2", "cvt2p3",
+    "lkw_bothoob", "lkw_ld1", "lkw_ld16", "lkw_ld17", "lkw_ldoob", "lkw_st1", "lkw_st16", "lkw_st17", "lkw_st19",
+    "lkw_st3")}
+
+
 def build(name):
+    if name in RETIRED:
+        raise SystemExit(f"{name}: retired, applies to the tree at {RETIRED[name]} "
+                         f"(git worktree add /tmp/wt {RETIRED[name]}; run this tool there)")
     dst = os.path.join(ROOT, "tools", f"{name}_lab")
     if os.path.exists(dst):
         shutil.rmtree(dst)
@@ -787,7 +799,7 @@ def check():
     srcs = {f: open(os.path.join(csrc, f)).read() for f in os.listdir(csrc) if f.endswith((".hip", ".h"))}
     bad = []
     for name in sorted(set(PATCHES) | set(COMBOS)):
-        if name.endswith("_") and name not in COMBOS:   # a component of combos only
+        if (name.endswith("_") and name not in COMBOS) or name in RETIRED:   # a combo component; retired
             continue
         s = dict(srcs)
         diffs = sorted({d for n in COMBOS.get(name, [name]) for pre, d in PREDIFF.items() if n.startswith(pre)})
@@ -816,7 +828,8 @@ def check():
 if __name__ == "__main__":
     if sys.argv[1:] == ["--check"]:
         bad = check()
-        print(f"{len(set(PATCHES) | set(COMBOS))} recipes, {len(bad)} stale" + (": " + " ".join(bad) if bad else ""))
+        print(f"{len(set(PATCHES) | set(COMBOS))} recipes ({len(RETIRED)} retired), {len(bad)} stale"
+              + (": " + " ".join(bad) if bad else ""))
         sys.exit(1 if bad else 0)
     for n in sys.argv[1:]:
         build(n)
