@@ -751,6 +751,16 @@ COMBOS["vx_sortonly"] = ["vx_nofold_", "vx_norank_", "vx_noreorder_"]
 # the gather's loads only: the window's copies read, nothing counted
 PATCHES["vx_loadonly_"] = [("voxel.hip", "        atomicAdd(&L.off[run_of(ev)], 1);", "        if (ev.x == 12345.f) atomicAdd(&L.off[0], 1);")]
 COMBOS["vx_loadonly"] = ["vx_nofold_", "vx_norank_", "vx_noreorder_", "vx_noplace_", "vx_loadonly_"]
+# operand pass (timing only): no panel stores (the split still computed; a never-true test keeps it)
+# / no fmap loads (values from the pixel index; the stores kept)
+_PK_ST = """        *reinterpret_cast<halfx8*>(p) = h0;
+        *reinterpret_cast<halfx8*>(p + k8) = h1;
+        *reinterpret_cast<halfx8*>(p + 1024) = l0;
+        *reinterpret_cast<halfx8*>(p + 1024 + k8) = l1;
+"""
+PATCHES["pk_nostore"] = [("build.hip", _PK_ST, "        if (h0[0] == (_Float16)12345.0f && l1[7] == (_Float16)-3.0f) {\n" + _PK_ST + "        }\n")]
+PATCHES["pk_noload"] = [("build.hip", "                v[i][kk] = (pix >= 0 && k < D) ? px[(int64_t)k * N] : 0.f;",
+                         "                v[i][kk] = (pix >= 0 && k < D) ? (float)(pix + k) : 0.f;")]
 # bitwise: 384 window events in LDS (more tiles per CU, more windows on the arena path)
 PATCHES["vx_cap384"] = [("voxel.hip", "constexpr int VB_CAP = 512;", "constexpr int VB_CAP = 384;")]
 
