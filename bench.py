@@ -422,8 +422,8 @@ def measure_upsample(B, H, W, device, reps=5):
 
 def measure_voxel(device, n=1_000_000, C=15, H=480, W=640, reps=5):
     """DSEC event -> voxel grid (dsec_utils.py:26-64) for one 100 ms window of
-    n synthetic events at full resolution, normalized -- ours (voxel.hip: prep, stable radix sort,
-    ordered gather, normalization) vs the reference's ATen op sequence (oracle/torch_ref.py) on this
+    n synthetic events at full resolution, normalized -- ours (voxel.hip: tile windows, a counting
+    sort in LDS, ordered gather, normalization) vs the reference's ATen op sequence (oracle/torch_ref.py) on this
     GPU and on one host core (main.py pins torch to one thread)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import torch_ref
@@ -469,6 +469,58 @@ def measure_voxel(device, n=1_000_000, C=15, H=480, W=640, reps=5):
             "speedup_vs_reference_gpu": round(ref_gpu / ours, 2),
             "note": "accumulated grid bit-exact with the reference's serial fold (the reference on a "
                     "GPU uses float atomics: not reproducible); normalization within 1e-6"}
+
+
+def measure_voxel_mvsec(device, n=300_000, C=15, H=260, W=346, reps=5):
+    """SURVEY §8f row 3, MVSEC form: EventSequenceToVoxelGrid_Pytorch (transformers.py:36-126) on
+    n synthetic events [n, 4] float64 already on the device (the reference moves a numpy array
+    there first; both legs here start from the device tensor), normalized -- ours (voxel.hip's
+    key-range counting sort and ordered gather, bit-exact) vs the reference's ATen ops
+    (oracle/torch_ref.py: index_add_ with float atomics) on this GPU and on one host core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch_ref
+    import eraft_amd
+    g = torch.Generator(device=device).manual_seed(9)
+    t = torch.sort(torch.rand((n,), generator=g, device=device, dtype=torch.float64)).values * 0.05 + 1.4e9
+    ev = torch.stack([t, torch.floor(torch.rand((n,), generator=g, device=device, dtype=torch.float64) * W),
+                      torch.floor(torch.rand((n,), generator=g, device=device, dtype=torch.float64) * H),
+                      (torch.rand((n,), generator=g, device=device) < 0.5).double()], 1).contiguous()
+
+    class _Seq:
+        features, image_width, image_height = ev, W, H
+    conv = eraft_amd.EventSequenceToVoxelGrid_Pytorch(C, gpu=True, normalize=True)
+    stream = torch.cuda.current_stream(device)
+
+    def gpu_ms(fn):
+        ts = []
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return sorted(ts[1:])[len(ts[1:]) // 2]
+
+    ours = gpu_ms(lambda: conv(_Seq))
+    ref_gpu = gpu_ms(lambda: torch_ref.voxel_grid_mvsec(ev, C, H, W))
+    evc = ev.cpu()
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    t0 = time.perf_counter()
+    torch_ref.voxel_grid_mvsec(evc, C, H, W)
+    ref_cpu = (time.perf_counter() - t0) * 1e3
+    torch.set_num_threads(nt)
+    nbytes = 32.0 * n + 4.0 * C * H * W   # the events in (4 x fp64) + the grid out
+    gbs = nbytes / (ours * 1e-3) / 1e9
+    return {"ms_per_call": round(ours, 4), "events": n, "grid": [C, H, W],
+            "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "work_per_launch": f"{nbytes:.4g} B (events in + grid out)",
+            "reference_ops_on_gpu_ms": round(ref_gpu, 3), "reference_ops_on_1_cpu_core_ms": round(ref_cpu, 1),
+            "speedup_vs_reference_gpu": round(ref_gpu / ours, 2),
+            "note": "includes the wrapper's out-of-range check (one host sync, as the reference's index_add_ "
+                    "raises); accumulated grid bit-exact with the reference's serial index_add_"}
 
 
 def shape_key(B, D, H, W, q):
@@ -1018,7 +1070,8 @@ def main():
             res["next_rows"] = {"lookup_conv1x1_relu": measure_fused_convc1(make_block(), coords, B, H, W, device),
                                 "forward_interpolate": measure_forward_interpolate(B, H, W, device),
                                 "upsample_flow": measure_upsample(B, H, W, device),
-                                "voxel_grid_dsec": measure_voxel(device)}
+                                "voxel_grid_dsec": measure_voxel(device),
+                                "voxel_grid_mvsec": measure_voxel_mvsec(device)}
     if a.mode == "batch" and world == 1 and not a.no_next and not a.no_e2e and (H, W) == (60, 80):
         res["e2e"] = measure_e2e(B, iters, device)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -110,3 +110,36 @@ def voxel_grid_dsec(events, C, H, W, normalize=True):
             mean, std = grid[nz].mean(), grid[nz].std()
             grid[nz] = (grid[nz] - mean) / std if std > 0 else grid[nz] - mean
     return grid
+
+
+def voxel_grid_mvsec(events, C, H, W, normalize=True):
+    """utils/transformers.py:36-126 (EventSequenceToVoxelGrid_Pytorch.__call__) on an [N, 4] float64
+    (t, x, y, p) tensor already on its device, same ATen ops in the same order (the reference moves
+    a numpy array to the device first; timed callers pass the device tensor)."""
+    ev = events.clone()
+    grid = torch.zeros(C, H, W, dtype=torch.float32, device=ev.device).flatten()
+    last, first = ev[-1, 0], ev[0, 0]
+    dt = last - first
+    if dt == 0:
+        dt = 1.0
+    ev[:, 0] = (C - 1) * (ev[:, 0] - first) / dt
+    ts, xs, ys = ev[:, 0], ev[:, 1].long(), ev[:, 2].long()
+    pols = ev[:, 3].float()
+    pols[pols == 0] = -1
+    tis = torch.floor(ts)
+    tis_long = tis.long()
+    dts = ts - tis
+    vals_left = pols * (1.0 - dts.float())
+    vals_right = pols * dts.float()
+    valid = (tis < C) & (tis >= 0)
+    grid.index_add_(0, xs[valid] + ys[valid] * W + tis_long[valid] * W * H, vals_left[valid])
+    valid = ((tis + 1) < C) & (tis >= 0)
+    grid.index_add_(0, xs[valid] + ys[valid] * W + (tis_long[valid] + 1) * W * H, vals_right[valid])
+    grid = grid.view(C, H, W)
+    if normalize:
+        nz = torch.nonzero(grid, as_tuple=True)
+        if nz[0].size()[0] > 0:
+            mean, std = grid[nz].mean(), grid[nz].std()
+            grid[nz] = (grid[nz] - mean) / std if std > 0 else grid[nz] - mean
+    return grid
+

@@ -49,3 +49,24 @@ def test_torch_ref_voxel_matches_reference():
                 assert oracle.same_bits(got, z[f"{k}/norm{norm}"]), (k, norm)
     finally:
         torch.set_num_threads(os.cpu_count() or 1)
+
+
+def test_torch_ref_voxel_mvsec_matches_reference():
+    """oracle/torch_ref.voxel_grid_mvsec (the bench's MVSEC reference leg) against the reference's
+    own outputs: bit-exact accumulated and normalized grids; the out-of-range event raises."""
+    from voxel_cases import MVSEC_VOXEL, mvsec_case
+    import torch_ref
+    z = np.load(os.path.join(GOLDEN, "next_voxel.npz"))
+    torch.set_num_threads(1)
+    try:
+        for k, (n, C, H, W, seed) in MVSEC_VOXEL.items():
+            ev = torch.from_numpy(mvsec_case(k, n, H, W, seed))
+            if f"{k}/raises" in z.files:
+                with pytest.raises((IndexError, RuntimeError)):
+                    torch_ref.voxel_grid_mvsec(ev, C, H, W, True)
+                continue
+            for norm in (0, 1):
+                got = torch_ref.voxel_grid_mvsec(ev, C, H, W, bool(norm)).numpy()
+                assert oracle.same_bits(got, z[f"{k}/norm{norm}"]), (k, norm)
+    finally:
+        torch.set_num_threads(os.cpu_count() or 1)
