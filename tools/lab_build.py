@@ -761,6 +761,12 @@ _PK_ST = """        *reinterpret_cast<halfx8*>(p) = h0;
 PATCHES["pk_nostore"] = [("build.hip", _PK_ST, "        if (h0[0] == (_Float16)12345.0f && l1[7] == (_Float16)-3.0f) {\n" + _PK_ST + "        }\n")]
 PATCHES["pk_noload"] = [("build.hip", "                v[i][kk] = (pix >= 0 && k < D) ? px[(int64_t)k * N] : 0.f;",
                          "                v[i][kk] = (pix >= 0 && k < D) ? (float)(pix + k) : 0.f;")]
+# operand pass (timing + accuracy probe, not bitwise): the split's lo halves rounded down to 8 / 6
+# significant bits (fewer toggling multiplier bits in the lo.hi / hi.lo MFMAs of a power-limited GEMM)
+PATCHES["lo8"] = [("build.hip", "        lo[j] = (_Float16)(x - (float)h);",
+                   "        lo[j] = (_Float16)__uint_as_float(__float_as_uint(x - (float)h) & 0xFFFF0000u);")]
+PATCHES["lo6"] = [("build.hip", "        lo[j] = (_Float16)(x - (float)h);",
+                   "        lo[j] = (_Float16)__uint_as_float(__float_as_uint(x - (float)h) & 0xFFFC0000u);")]
 # bitwise: 384 window events in LDS (more tiles per CU, more windows on the arena path)
 PATCHES["vx_cap384"] = [("voxel.hip", "constexpr int VB_CAP = 512;", "constexpr int VB_CAP = 384;")]
 
