@@ -85,7 +85,8 @@ def test_voxel_mvsec_full_res_vs_oracle(ea):
     assert not bad and oracle.same_bits(g, ref)
 
 
-@pytest.mark.parametrize("case", ["hot_pixel", "dense_ragged", "sparse_ragged", "unsorted_t"])
+@pytest.mark.parametrize("case", ["hot_pixel", "dense_ragged", "sparse_ragged", "unsorted_t", "c23_run_table_full",
+                                  "c24_key_range_fallback"])
 def test_voxel_dsec_tiled_paths_vs_oracle(ea, case):
     """The tiled DSEC path (round 6): 4 x 16 cell tiles, each reading its window (its base cells and
     the +1 halo, every time bin) from one contiguous bucket -- in LDS, or past VB_CAP = 512 events
@@ -93,8 +94,9 @@ def test_voxel_dsec_tiled_paths_vs_oracle(ea, case):
     base cell (~12,000 in one window: the arena, runs of thousands ranked by event index);
     dense_ragged: every window past the cap (~1,800 events each), tiles cut by H % 4 and W % 16;
     sparse_ragged: the LDS path on partial tiles; unsorted_t: timestamps not in order (a bucket then
-    interleaves bins' events arbitrarily).  Accumulated grid bit-exact with the serial fold,
-    normalized within NORM_TOL."""
+    interleaves bins' events arbitrarily); C = 23: the run table full (2,040 of 2,048), C = 24: the
+    key-range pipeline instead.  Accumulated grid bit-exact with the serial fold, normalized within
+    NORM_TOL."""
     if case == "hot_pixel":
         n, C, H, W = 20_000, 3, 16, 64
         p, t, x, y = prng.dsec_events(730, n, H, W)
@@ -107,10 +109,14 @@ def test_voxel_dsec_tiled_paths_vs_oracle(ea, case):
     elif case == "sparse_ragged":
         n, C, H, W = 3_000, 5, 21, 70
         p, t, x, y = prng.dsec_events(750, n, H, W)
-    else:
+    elif case == "unsorted_t":
         n, C, H, W = 8_000, 4, 30, 90
         p, t, x, y = prng.dsec_events(760, n, H, W)
         t = t[np.argsort(prng.uniform(761, (n,)))].copy()   # a permutation: t[0], t[-1] arbitrary
+    else:   # (C + 1) * 85 runs per window: 2,040 at C = 23 (the LDS table's last fit), C = 24 the fallback
+        n, H, W = 20_000, 13, 37
+        C = 23 if case == "c23_run_table_full" else 24
+        p, t, x, y = prng.dsec_events(770 + C, n, H, W)
     g = _dsec(ea, p, t, x, y, C, H, W, False)
     assert oracle.same_bits(g, oracle.voxel_dsec(p, t, x, y, C, H, W, False)), case
     np.testing.assert_allclose(_dsec(ea, p, t, x, y, C, H, W, True), oracle.voxel_dsec(p, t, x, y, C, H, W, True),
