@@ -767,8 +767,9 @@ PATCHES["lo8"] = [("build.hip", "        lo[j] = (_Float16)(x - (float)h);",
                    "        lo[j] = (_Float16)__uint_as_float(__float_as_uint(x - (float)h) & 0xFFFF0000u);")]
 PATCHES["lo6"] = [("build.hip", "        lo[j] = (_Float16)(x - (float)h);",
                    "        lo[j] = (_Float16)__uint_as_float(__float_as_uint(x - (float)h) & 0xFFFC0000u);")]
-# bitwise: 384 window events in LDS (more tiles per CU, more windows on the arena path)
-PATCHES["vx_cap384"] = [("voxel.hip", "constexpr int VB_CAP = 512;", "constexpr int VB_CAP = 384;")]
+# voxel count blocks (bitwise): 512 threads x 8 events (245 blocks at 1M events) / 1024 x 4 (245)
+PATCHES["vx_cnt512"] = [("voxel.hip", "constexpr int VB_CNT = 1024, VB_EPB = 8 * VB_CNT;", "constexpr int VB_CNT = 512, VB_EPB = 8 * VB_CNT;")]
+PATCHES["vx_epb4"] = [("voxel.hip", "constexpr int VB_CNT = 1024, VB_EPB = 8 * VB_CNT;", "constexpr int VB_CNT = 1024, VB_EPB = 4 * VB_CNT;")]
 
 PREDIFF = {"qs": "build_qs.diff", "lkw_": "lookup_win.diff", "mo_ws": "lookup_conv_ws.diff", "cvq": "conv_tiles.diff",
            "cvt": "conv_tiles.diff"}
