@@ -78,13 +78,25 @@ class CorrBlock:
             raise RuntimeError("fmap1/fmap2 must be contiguous (reference: view size is not "
                                "compatible with input tensor's size and stride)")
         B, D, H, W = fmap1.shape
+        # degenerate shapes as the reference (tests/golden/degenerate.npz): an empty batch or map
+        # raises where its reshape / avg_pool2d do (corr.py:16-24); D = 0 feature channels give
+        # 0 / sqrt(0) = NaN volumes, which its lookup samples like any other values
+        if B == 0:
+            raise RuntimeError(f"cannot reshape tensor of 0 elements into shape [0, {H}, {W}, -1] "
+                               "(empty batch: the reference's CorrBlock.corr reshape)")
+        if H == 0 or W == 0:
+            raise RuntimeError(f"Expected 3D or 4D (batch mode) tensor with optional 0 dim batch size for "
+                               f"input, but got:[{B * H * W}, 1, {H}, {W}] (empty map: the reference's avg_pool2d)")
         self._shape = (B, D, H, W)
         self._device = fmap1.device
         Q = H * W
         self._h, self._w, self._off = _lib.layout(B * Q, H, W, num_levels)
         with _lib.on_device(self._device):
-            self._pyramid = _lib.build_pyramid(fmap1, fmap2, B, D, H, W, Q, num_levels, self._off,
-                                               "CorrBlock build")
+            if D == 0:
+                self._pyramid = torch.full((self._off[-1],), float("nan"), dtype=torch.float32, device=self._device)
+            else:
+                self._pyramid = _lib.build_pyramid(fmap1, fmap2, B, D, H, W, Q, num_levels, self._off,
+                                                   "CorrBlock build")
         self._rows = B * Q
         self._levels_cache = None
         self._wcache = {}   # packed convc1 weights of this block (_lib.packed_conv1x1_weight)

@@ -266,3 +266,19 @@ def test_golden_pair_staging(ea, name, L):
     for s in [k[len("coords_"):] for k in z if k.startswith("coords_")]:
         got = _lookup_on(ea, levels, z[f"coords_{s}"], r)
         assert oracle.same_bits(got, z[f"out_{s}"][:, :L * K * K]), s
+
+
+def test_degenerate_shapes_as_reference(ea):
+    """tests/golden/degenerate.npz (make_golden_degenerate.py): D = 0 features -> the reference's
+    NaN volumes, sampled bit for bit (NaN where a corner lies inside a level, 0 where none does);
+    an empty batch or map raises RuntimeError as the reference's reshape / avg_pool2d do."""
+    z = np.load(os.path.join(GOLDEN, "degenerate.npz"))
+    coords = torch.from_numpy(z["d0/coords"]).to(DEV)
+    B, _, H, W = coords.shape
+    f = torch.zeros((B, 0, H, W), device=DEV)
+    with torch.no_grad():
+        got = ea.CorrBlock(f, f.clone(), num_levels=2, radius=1)(coords).cpu().numpy()
+    assert oracle.same_bits(got, z["d0/out"])
+    for shape in ((0, 8, H, W), (2, 8, 0, W)):
+        with pytest.raises(RuntimeError):
+            ea.CorrBlock(torch.zeros(shape, device=DEV), torch.zeros(shape, device=DEV), num_levels=2, radius=1)
